@@ -1,0 +1,255 @@
+#!/usr/bin/env python
+"""bench.py — single-batch decode throughput of the MI355X path (BASELINE.json metric).
+
+metric: decode tok/s + %HBM-roofline, Mistral-7B fp16, 1x MI355X vs -d cpu.
+
+A "step" is one greedy decode token: argmax over the logits + one full forward pass
+(embed -> 32 layers -> final norm -> lm_head), replayed from a hipGraph by the device-side
+decode loop (xh_decode_greedy).  Workload (BASELINE configs[1]): Mistral-7B-Instruct-v0.2
+shapes, fp16 weights, 4k context, a 32-token prompt (BOS + LCG ids) hydrated first, then
+`--warmup` untimed and `--steps` timed decode tokens.  Weights are synthetic (no checkpoints
+offline): generated on the device from include/xalm_synth.h; the CPU baseline builds the
+bit-identical host copy and runs the C oracle (the reference's CPU algorithm restated).
+
+Multi-GPU: the path does not shard -> N independent replicas, one process per
+GPU, no collective on the data path; value = total tokens of all ranks / max rank time.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from xalm_amd import _lib as L  # noqa: E402
+from xalm_amd.model import InferenceState, Model  # noqa: E402
+
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+WORKLOADS = {
+    # BASELINE.json configs[1]
+    "mistral-7b-f16": dict(desc="Mistral-7B-Instruct-v0.2 fp16, greedy decode, 4k context (configs[1])",
+                           dim=4096, hidden=14336, layers=32, heads=32, kv_heads=8, head_dim=128, vocab=32000,
+                           msl=4096, theta=1e6, wdt=L.F16, edt=L.F16, cdt=L.F16, dtype="f16", kv_prefill=0),
+    # configs[2]: fp8 matrices, embed/lm_head boosted to bf16 (convert.py:729-768)
+    "mistral-7b-f8": dict(desc="Mistral-7B fp8 e4m3 weights (embed/lm_head bf16), greedy decode, 4k context (configs[2])",
+                          dim=4096, hidden=14336, layers=32, heads=32, kv_heads=8, head_dim=128, vocab=32000,
+                          msl=4096, theta=1e6, wdt=L.F8_E4M3, edt=L.BF16, cdt=L.BF16, dtype="f8_e4m3", kv_prefill=0),
+    # configs[3]: -T 32768, KV ring pre-filled, decode at pos >= 32767 (KV-dominated)
+    "mistral-7b-f16-32k": dict(desc="Mistral-7B fp16, -T 32768, KV ring full (configs[3])",
+                               dim=4096, hidden=14336, layers=32, heads=32, kv_heads=8, head_dim=128, vocab=32000,
+                               msl=32768, theta=1e6, wdt=L.F16, edt=L.F16, cdt=L.F16, dtype="f16",
+                               kv_prefill=32767),
+    # configs[4]
+    "llama3-8b-f16": dict(desc="Llama-3-8B fp16, greedy decode, 4k context (configs[4])",
+                          dim=4096, hidden=14336, layers=32, heads=32, kv_heads=8, head_dim=128, vocab=128256,
+                          msl=4096, theta=5e5, wdt=L.F16, edt=L.F16, cdt=L.F16, dtype="f16", kv_prefill=0),
+}
+
+
+def make_config(w):
+    c = L.XhConfig()
+    c.dim, c.hidden_dim, c.head_dim, c.n_layers = w["dim"], w["hidden"], w["head_dim"], w["layers"]
+    c.n_heads, c.n_kv_heads, c.vocab_size, c.max_seq_len = w["heads"], w["kv_heads"], w["vocab"], w["msl"]
+    c.rope_theta, c.rotary_dim, c.norm_eps, c.act = w["theta"], w["head_dim"], 1e-5, L.ACT_SILU
+    c.qkv_clip = float(np.finfo(np.float32).max)
+    c.tie_word_embeddings = 0
+    return c
+
+
+def tensor_specs(w):
+    """(kind, layer, dtype, seed, mean, std) of every tensor; SURVEY §8d synthetic recipe:
+    matrices N(0,0.02^2), norms 1+N(0,0.01^2) bf16, embedding rows N(0,1)."""
+    specs = [(L.EMBED, 0, w["edt"], 1001, 0.0, 1.0), (L.FINAL_NORM, 0, L.BF16, 1002, 1.0, 0.01),
+             (L.WCLS, 0, w["cdt"], 1003, 0.0, 0.02)]
+    for layer in range(w["layers"]):
+        base = 10_000 + 100 * layer
+        specs += [(L.ATTN_NORM, layer, L.BF16, base + 1, 1.0, 0.01), (L.FFN_NORM, layer, L.BF16, base + 2, 1.0, 0.01)]
+        for k in (L.WQ, L.WK, L.WV, L.WO, L.W1, L.W2, L.W3):
+            specs.append((k, layer, w["wdt"], base + 10 + k, 0.0, 0.02))
+    return specs
+
+
+def tensor_shape(c, kind):
+    q_dim, kv_dim = c.n_heads * c.head_dim, c.n_kv_heads * c.head_dim
+    return {L.EMBED: (c.vocab_size, c.dim), L.WCLS: (c.vocab_size, c.dim), L.FINAL_NORM: (1, c.dim),
+            L.ATTN_NORM: (1, c.dim), L.FFN_NORM: (1, c.dim), L.WQ: (q_dim, c.dim), L.WK: (kv_dim, c.dim),
+            L.WV: (kv_dim, c.dim), L.WO: (c.dim, q_dim), L.W1: (c.hidden_dim, c.dim),
+            L.W2: (c.dim, c.hidden_dim), L.W3: (c.hidden_dim, c.dim)}[kind]
+
+
+def prompt_tokens(vocab, n=32, seed=7):
+    out, s = [1], seed
+    for _ in range(n - 1):
+        s = (1103515245 * s + 12345) & 0x7FFFFFFF
+        out.append(3 + s % (vocab - 3))
+    return out
+
+
+def sync_all(dist, torch_mod):
+    if torch_mod is not None and torch_mod.cuda.is_available():
+        torch_mod.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+
+
+def cpu_baseline(w, c, prompt, gpu_logits0, gpu_tokens, n_decode):
+    """Oracle (restated src/infer.cpp, OpenMP) on the same weights, bounded sample."""
+    from oracle import oracle as O
+    t_gen = time.time()
+    om = O.OracleModel(c)
+    for kind, layer, dt, seed, mean, std in tensor_specs(w):
+        rows, cols = tensor_shape(c, kind)
+        om.set_tensor(kind, layer, dt, O.synthetic(rows, cols, dt, seed, mean, std))
+    if w["kv_prefill"]:
+        return None  # the CPU sample is defined on the 4k-context workloads only
+    t_gen = time.time() - t_gen
+    for pos, tok in enumerate(prompt):
+        om.forward(tok, pos, L.OUTPUT_LOGITS if pos == len(prompt) - 1 else L.HYDRATE_KV_CACHE)
+    lg0 = om.logits()
+    parity_max_abs = float(np.abs(lg0 - gpu_logits0).max())
+    # teacher-forced on the GPU's tokens so both sides see identical inputs
+    pos = len(prompt)
+    agree = 0
+    t0 = time.time()
+    for i in range(n_decode):
+        agree += int(O.sample_argmax(om.logits()) == gpu_tokens[i])
+        om.forward(gpu_tokens[i], pos, L.OUTPUT_LOGITS)
+        pos += 1
+    dt = time.time() - t0
+    return dict(value=n_decode / dt, unit="tok/s", cores=O.num_threads(), kind="port",
+                sample=f"{n_decode} greedy decode tokens after a {len(prompt)}-token hydrate, full "
+                       f"{w['desc'].split(',')[0]} shapes, same synthetic weights (wall clock, "
+                       f"OpenMP oracle/xalm_oracle.c)",
+                ms_per_token=1000 * dt / n_decode, weight_gen_s=round(t_gen, 2),
+                parity={"logits_max_abs_after_prompt": parity_max_abs,
+                        "logits_scale": float(np.abs(lg0).max()),
+                        "greedy_tokens_agree": f"{agree}/{n_decode}"})
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=256)
+    ap.add_argument("--warmup", type=int, default=8)
+    ap.add_argument("--workload", default="mistral-7b-f16", choices=sorted(WORKLOADS))
+    ap.add_argument("--cpu-tokens", type=int, default=4)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--kernel-iters", type=int, default=200)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    torch_mod = None
+    try:
+        import torch as torch_mod  # noqa: F811  (plumbing: barrier + device sync only)
+    except ImportError:
+        torch_mod = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    w = WORKLOADS[args.workload]
+    c = make_config(w)
+    model = Model(c, device=local_rank)
+    for kind, layer, dt, seed, mean, std in tensor_specs(w):
+        model.upload_synthetic(kind, layer, dt, seed, mean, std)
+
+    prompt = prompt_tokens(c.vocab_size)
+    st = InferenceState(c)
+    pos0 = 0
+    if w["kv_prefill"]:
+        # configs[3]: ring slots 0..kv_prefill-1 hold history; decode continues at pos = kv_prefill
+        for layer in range(c.n_layers):
+            model.kv_fill_synthetic(layer, 0, 0, w["kv_prefill"], 5000 + 2 * layer, 1.0)
+            model.kv_fill_synthetic(layer, 1, 0, w["kv_prefill"], 5001 + 2 * layer, 1.0)
+        pos0 = w["kv_prefill"]
+    for i, tok in enumerate(prompt[:1] if w["kv_prefill"] else prompt):
+        last = w["kv_prefill"] or i == len(prompt) - 1
+        model.forward(st, tok, pos0 + i, L.OUTPUT_LOGITS if last else L.HYDRATE_KV_CACHE)
+    pos = pos0 + (1 if w["kv_prefill"] else len(prompt))
+    logits0 = st.logits().copy()
+
+    warm_tokens = model.decode_greedy(pos, args.warmup) if args.warmup else []
+    pos += args.warmup
+    if pos + args.steps > c.max_seq_len and not w["kv_prefill"]:
+        raise SystemExit(f"steps exceed the {c.max_seq_len} context")
+
+    sync_all(dist, torch_mod)
+    t0 = time.perf_counter()
+    toks = model.decode_greedy(pos, args.steps)
+    sync_all(dist, torch_mod)
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        dist.barrier()
+    assert len(toks) == args.steps
+
+    # algorithmic bytes of the timed tokens: Model::active_bytes(pos) (src/model.cpp:12-35)
+    step_bytes = sum(model.active_bytes(p) for p in range(pos, pos + args.steps))
+    step_gbps = step_bytes / elapsed / 1e9
+
+    # dominant kernel: fused gate/up matvec (W1/W3 = 44 % of the bytes), timed on its own stream
+    kv_len_now = min(c.max_seq_len, pos + args.steps)
+    k_us = model.time_kernel(0, args.kernel_iters)
+    k_bytes = model.kernel_bytes(0, kv_len_now)
+    k_gbps = k_bytes / (k_us * 1e-6) / 1e9
+    extra_kernels = {}
+    for which, name in ((1, "gemv_qkv"), (2, "gemv_wo"), (3, "gemv_w2"), (4, "gemv_lm_head"), (5, "attention")):
+        us = model.time_kernel(which, max(20, args.kernel_iters // 4))
+        b = model.kernel_bytes(which, kv_len_now)
+        extra_kernels[name] = {"avg_us": round(us, 2), "GBps": round(b / (us * 1e-6) / 1e9, 1)}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not w["kv_prefill"]:
+        n = min(args.cpu_tokens, len(warm_tokens)) if warm_tokens else 0
+        if n:
+            cpu = cpu_baseline(w, c, prompt, logits0, warm_tokens, n)
+
+    value = world * args.steps / elapsed
+    if rank == 0:
+        out = {
+            "metric": "decode tok/s + %HBM-roofline, Mistral-7B fp16, 1xMI355X vs -d cpu",
+            "value": round(value, 2),
+            "unit": "tok/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1000 * elapsed / args.steps, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": w["dtype"],
+            "data": "synthetic (deterministic xalm_synth weights of the named shapes; no checkpoint offline)",
+            "config": {"workload": w["desc"], "prompt_tokens": len(prompt), "max_seq_len": c.max_seq_len,
+                       "kv_len_timed": [pos + 1, pos + args.steps], "batch": 1, "parallelism": f"replicas x{world}"},
+            "roofline": {"bound": "hbm", "achieved": round(k_gbps, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": round(k_gbps / HBM_PEAK_GBPS, 4), "traffic": None,
+                         "kernel": "gemv_kernel<PRO_RMSNORM,EPI_GLU> (fused W1/W3 + rmsnorm + silu*up), layer 0",
+                         "bytes_per_launch": k_bytes, "avg_launch_us": round(k_us, 2)},
+            "hbm_step": {"achieved_GBps": round(step_gbps, 1), "frac": round(step_gbps / HBM_PEAK_GBPS, 4),
+                         "bytes_per_token": step_bytes // args.steps,
+                         "note": "Model::active_bytes per token x tok/s, whole forward incl. launch gaps"},
+            "kernels": extra_kernels,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    model.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,471 @@
+/*
+ * xalm_oracle.c — CPU restatement of jubruckne/Xalm's forward pass (TEST INFRASTRUCTURE).
+ *
+ * Every function cites the reference file:line it restates.  Semantics follow the ARM
+ * build the reference targets (bf16 norm weights are decoded to f32).
+ * This file is the checker for the HIP path and the timed `-d cpu` baseline; nothing in
+ * the product links it (see xalm_oracle.h).
+ *
+ * Build: oracle/Makefile  (gcc -O3 -fopenmp -mavx2 -mfma -mf16c)
+ */
+#include "xalm_oracle.h"
+
+#include <float.h>
+#include <math.h>
+#include <omp.h>
+#include <stdlib.h>
+#include <string.h>
+
+#if defined(__F16C__) && defined(__AVX2__) && defined(__FMA__)
+#include <immintrin.h>
+#define XO_SIMD 1
+#endif
+
+#include "../include/xalm_synth.h"
+
+#define KV_SINKS 2 /* src/model.h:10 */
+
+/* Host copy of the device synthetic weights (xh_upload_synthetic): same header, same bits.
+ * dst is a dense [rows][cols] tensor of `dtype`. */
+void xo_fill_synthetic(void* dst, size_t rows, size_t cols, int dtype, uint64_t seed, float mean, float std) {
+    const size_t n = rows * cols;
+    size_t i;
+#pragma omp parallel for schedule(static)
+    for (i = 0; i < n; i++) xs_store(dst, i, dtype, xs_value(seed, i, mean, std));
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* element decode, src/types.h                                                          */
+/* ------------------------------------------------------------------------------------ */
+static inline float bits_f32(uint32_t u) { float f; memcpy(&f, &u, 4); return f; }
+static inline uint32_t f32_bits(float f) { uint32_t u; memcpy(&u, &f, 4); return u; }
+
+/* IEEE binary16 -> binary32 (exact). ARM `float16_t` promotion. */
+float xo_f16_to_f32(uint16_t h) {
+    const uint32_t s = (uint32_t)(h & 0x8000u) << 16;
+    const uint32_t e = (h >> 10) & 0x1fu;
+    const uint32_t m = h & 0x3ffu;
+    if (e == 0) {
+        if (m == 0) return bits_f32(s);
+        const float v = (float)m * 5.9604644775390625e-08f; /* m * 2^-24, exact */
+        return s ? -v : v;
+    }
+    if (e == 31) return bits_f32(s | 0x7f800000u | (m << 13));
+    return bits_f32(s | ((e + 112u) << 23) | (m << 13));
+}
+
+/* binary32 -> binary16, round to nearest even (ARM fcvt; the KV-cache store
+ * `kb[...] = s.k()[i]`, src/infer.cpp:410-414). */
+uint16_t xo_f32_to_f16(float fv) {
+    const uint32_t f = f32_bits(fv);
+    const uint16_t h_sgn = (uint16_t)((f & 0x80000000u) >> 16);
+    uint32_t f_exp = f & 0x7f800000u;
+    uint32_t f_sig;
+    if (f_exp >= 0x47800000u) {
+        if (f_exp == 0x7f800000u) {
+            f_sig = f & 0x007fffffu;
+            if (f_sig != 0) {
+                uint16_t ret = (uint16_t)(0x7c00u + (f_sig >> 13));
+                if (ret == 0x7c00u) ret++;
+                return (uint16_t)(h_sgn + ret) | 0x0200u;
+            }
+        }
+        return (uint16_t)(h_sgn + 0x7c00u);
+    }
+    if (f_exp <= 0x38000000u) {
+        if (f_exp < 0x33000000u) return h_sgn;
+        f_exp >>= 23;
+        f_sig = 0x00800000u + (f & 0x007fffffu);
+        f_sig >>= (113u - f_exp);
+        if (((f_sig & 0x00003fffu) != 0x00001000u) || (f & 0x000007ffu)) f_sig += 0x00001000u;
+        return (uint16_t)(h_sgn + (uint16_t)(f_sig >> 13));
+    }
+    const uint16_t h_exp = (uint16_t)((f_exp - 0x38000000u) >> 13);
+    f_sig = f & 0x007fffffu;
+    if ((f_sig & 0x00003fffu) != 0x00001000u) f_sig += 0x00001000u;
+    return (uint16_t)(h_sgn + (uint16_t)((f_sig >> 13) + h_exp));
+}
+
+/* bf16_to_f32, src/types.h:322-325 */
+static inline float bf16_to_f32(uint16_t h) { return bits_f32((uint32_t)h << 16); }
+
+/* f8_t<E,M>::to_float, src/types.h:302-314: (sign<<24) | (bits&0x7F)<<(23-M), times
+ * 2^(127-bias) with bias = 2^(E-1)-1. */
+static inline float f8e4m3_to_f32(uint8_t b) {
+    const uint32_t u = ((uint32_t)(b & 0x80u) << 24) | ((uint32_t)(b & 0x7fu) << 20);
+    return bits_f32(u) * 0x1p120f;
+}
+static inline float f8e5m2_to_f32(uint8_t b) {
+    const uint32_t u = ((uint32_t)(b & 0x80u) << 24) | ((uint32_t)(b & 0x7fu) << 21);
+    return bits_f32(u) * 0x1p112f;
+}
+/* Type::Q8 get_float, src/types.h:423-424 */
+static inline float q8_to_f32(int8_t q) { return (1.f / 100.f) * (float)q; }
+
+float xo_decode(int dtype, const void* data, size_t idx) {
+    switch (dtype) {
+        case XH_F32: return ((const float*)data)[idx];
+        case XH_F16: return xo_f16_to_f32(((const uint16_t*)data)[idx]);
+        case XH_BF16: return bf16_to_f32(((const uint16_t*)data)[idx]);
+        case XH_F8_E4M3: return f8e4m3_to_f32(((const uint8_t*)data)[idx]);
+        case XH_F8_E5M2: return f8e5m2_to_f32(((const uint8_t*)data)[idx]);
+        case XH_Q8: return q8_to_f32(((const int8_t*)data)[idx]);
+        default: return NAN;
+    }
+}
+
+static size_t dtype_bits(int dtype) {
+    switch (dtype) {
+        case XH_F32: return 32;
+        case XH_F16: case XH_BF16: return 16;
+        case XH_F8_E4M3: case XH_F8_E5M2: case XH_U8: case XH_Q8: return 8;
+        default: return 0;
+    }
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* ops, src/infer.cpp                                                                    */
+/* ------------------------------------------------------------------------------------ */
+
+/* matmul<TX,TW>, src/infer.cpp:104-135 (dispatch :185-216): xout[i] = sum_j dec(W[i,j])*x[j],
+ * fp32 accumulate, OpenMP over rows (the reference's `omp simd` leaves the in-row order
+ * implementation-defined; here 8-wide FMA lanes for f16). */
+void xo_matmul(float* xout, const float* x, const void* w, const int dtype, const int n, const int d) {
+    int i;
+    if (dtype == XH_F16) {
+        const uint16_t* W = (const uint16_t*)w;
+#pragma omp parallel for schedule(static)
+        for (i = 0; i < d; i++) {
+            const uint16_t* row = W + (size_t)i * n;
+            int j = 0;
+            float val = 0.0f;
+#ifdef XO_SIMD
+            __m256 a0 = _mm256_setzero_ps(), a1 = _mm256_setzero_ps();
+            __m256 a2 = _mm256_setzero_ps(), a3 = _mm256_setzero_ps();
+            for (; j + 32 <= n; j += 32) {
+                a0 = _mm256_fmadd_ps(_mm256_cvtph_ps(_mm_loadu_si128((const __m128i*)(row + j))), _mm256_loadu_ps(x + j), a0);
+                a1 = _mm256_fmadd_ps(_mm256_cvtph_ps(_mm_loadu_si128((const __m128i*)(row + j + 8))), _mm256_loadu_ps(x + j + 8), a1);
+                a2 = _mm256_fmadd_ps(_mm256_cvtph_ps(_mm_loadu_si128((const __m128i*)(row + j + 16))), _mm256_loadu_ps(x + j + 16), a2);
+                a3 = _mm256_fmadd_ps(_mm256_cvtph_ps(_mm_loadu_si128((const __m128i*)(row + j + 24))), _mm256_loadu_ps(x + j + 24), a3);
+            }
+            __m256 s = _mm256_add_ps(_mm256_add_ps(a0, a1), _mm256_add_ps(a2, a3));
+            __m128 s4 = _mm_add_ps(_mm256_castps256_ps128(s), _mm256_extractf128_ps(s, 1));
+            s4 = _mm_hadd_ps(s4, s4);
+            s4 = _mm_hadd_ps(s4, s4);
+            val = _mm_cvtss_f32(s4);
+#endif
+            for (; j < n; j++) val += xo_f16_to_f32(row[j]) * x[j];
+            xout[i] = val;
+        }
+        return;
+    }
+#define XO_MATMUL_LOOP(T, DEC)                                              \
+    {                                                                       \
+        const T* W = (const T*)w;                                           \
+        _Pragma("omp parallel for schedule(static)")                        \
+        for (i = 0; i < d; i++) {                                           \
+            const T* row = W + (size_t)i * n;                               \
+            float val = 0.0f;                                               \
+            for (int j = 0; j < n; j++) val += DEC(row[j]) * x[j];          \
+            xout[i] = val;                                                  \
+        }                                                                   \
+    }
+#define DEC_F32(v) (v)
+    switch (dtype) {
+        case XH_F32: XO_MATMUL_LOOP(float, DEC_F32); break;
+        case XH_BF16: XO_MATMUL_LOOP(uint16_t, bf16_to_f32); break;
+        case XH_F8_E4M3: XO_MATMUL_LOOP(uint8_t, f8e4m3_to_f32); break;
+        case XH_F8_E5M2: XO_MATMUL_LOOP(uint8_t, f8e5m2_to_f32); break;
+        case XH_Q8: XO_MATMUL_LOOP(int8_t, q8_to_f32); break;
+        default: for (i = 0; i < d; i++) xout[i] = NAN; break;
+    }
+#undef XO_MATMUL_LOOP
+#undef DEC_F32
+}
+
+/* rmsnorm, src/infer.cpp:224-236 (dispatch :238-251): serial sum of squares in index
+ * order; o = x * (1/sqrtf(ss/n + eps)) * w.  Safe in place (o == x), as :628. */
+void xo_rmsnorm(float* o, const float* x, const void* w, const int dtype, const int size, const float eps) {
+    float rms = 0.0f;
+    for (int i = 0; i < size; ++i) rms += x[i] * x[i];
+    rms = sqrtf(rms / (float)size + eps);
+    const float scale = 1.0f / rms;
+    for (int i = 0; i < size; ++i) {
+        const float wi = dtype == XH_BF16 ? bf16_to_f32(((const uint16_t*)w)[i]) : ((const float*)w)[i];
+        o[i] = x[i] * scale * wi;
+    }
+}
+
+/* softmax, src/infer.cpp:280-297 */
+static void softmax(float* o, const float* x, const int size) {
+    float score_max = -FLT_MAX; /* std::numeric_limits<float>::lowest() */
+    for (int i = 0; i < size; ++i)
+        if (x[i] > score_max) score_max = x[i];
+    float score_sum = 0.0f;
+    for (int i = 0; i < size; ++i) {
+        o[i] = expf(x[i] - score_max);
+        score_sum += o[i];
+    }
+    for (int i = 0; i < size; ++i) o[i] /= score_sum;
+}
+
+/* gelu / silu / clip, src/infer.cpp:299-303 */
+static inline float gelu(const float x) { return 0.5f * x * (1.0f + tanhf(0.797885f * (x + 0.044715f * x * x * x))); }
+static inline float silu(const float x) { return x / (1.0f + expf(-x)); }
+static inline float clip(const float x, const float v) { return x < -v ? -v : (x > v ? v : x); }
+
+/* rope, src/infer.cpp:305-322: adjacent pairs (i, i+1) rotated by pos * theta^(-j/rot). */
+void xo_rope(float* vec, const int d, const int head_dim, const int pos, const float theta, const int rotary_dim) {
+    for (int i = 0; i < d; i += 2) {
+        const int j_head = i % head_dim;
+        const float freq = j_head >= rotary_dim ? 0.f : 1.0f / powf(theta, (float)j_head / (float)rotary_dim);
+        const float val = (float)pos * freq;
+        const float fcr = cosf(val);
+        const float fci = sinf(val);
+        const float v0 = vec[i];
+        const float v1 = vec[i + 1];
+        vec[i] = v0 * fcr - v1 * fci;
+        vec[i + 1] = v0 * fci + v1 * fcr;
+    }
+}
+
+/* attn, src/infer.cpp:325-359: one head over kv_len ring slots in slot order. */
+static void attn(float* xout, float* atth, const float* qh, const uint16_t* kh, const uint16_t* vh,
+                 const int head_dim, const int n_kv_heads, const int kv_len) {
+    const int kv_stride = n_kv_heads * head_dim;
+    const float sqrt_head_dim = 1.0f / sqrtf((float)head_dim);
+    for (int t = 0; t < kv_len; ++t) {
+        float score = 0.0f;
+        for (int i = 0; i < head_dim; ++i) score += qh[i] * xo_f16_to_f32(kh[(size_t)t * kv_stride + i]);
+        atth[t] = score * sqrt_head_dim;
+    }
+    softmax(atth, atth, kv_len);
+    for (int i = 0; i < head_dim; ++i) {
+        float vi = 0.0f;
+        for (int t = 0; t < kv_len; ++t) vi += atth[t] * xo_f16_to_f32(vh[(size_t)t * kv_stride + i]);
+        xout[i] = vi;
+    }
+}
+
+/* mha_cpu, src/infer.cpp:498-517 */
+void xo_mha(float* xout, float* att, const uint16_t* kb, const uint16_t* vb, const float* q, const int head_dim,
+            const int kv_len, const int max_seq_len, const int n_heads, const int n_kv_heads) {
+    const int q_per_kv_head = n_heads / n_kv_heads;
+    int h;
+#pragma omp parallel for schedule(static)
+    for (h = 0; h < n_heads; h++) {
+        const int kv_head_offset = (h / q_per_kv_head) * head_dim;
+        attn(xout + head_dim * h, att + (size_t)max_seq_len * h, q + head_dim * h, kb + kv_head_offset,
+             vb + kv_head_offset, head_dim, n_kv_heads, kv_len);
+    }
+}
+
+/* Sampler::sample_argmax, src/sampler.cpp:19-30 (max starts at FLT_MIN; first max wins) */
+int xo_sample_argmax(const float* logits, const int vocab) {
+    int argmax = 0;
+    float max_val = FLT_MIN;
+    for (int i = 0; i < vocab; ++i)
+        if (logits[i] > max_val) { max_val = logits[i]; argmax = i; }
+    return argmax;
+}
+
+/* Sampler::sample_prob, src/sampler.cpp:3-17 */
+float xo_sample_prob(const float* logits, const int vocab, const int index) {
+    float max_val = FLT_MIN;
+    for (int i = 0; i < vocab; ++i)
+        if (logits[i] > max_val) max_val = logits[i];
+    float sum = 0;
+    for (int i = 0; i < vocab; ++i) sum += expf(logits[i] - max_val);
+    return expf(logits[index] - max_val) / sum;
+}
+
+int xo_num_threads(void) { return omp_get_max_threads(); }
+
+/* ------------------------------------------------------------------------------------ */
+/* model + InferenceState, src/model.h:96-284, src/model.cpp                             */
+/* ------------------------------------------------------------------------------------ */
+typedef struct { int dtype; const void* data; } xo_tensor;
+
+typedef struct {
+    xo_tensor t[XH_NUM_KINDS];
+    uint16_t* key_cache;   /* float16_t[max_seq_len * kv_dim], src/model.cpp:102-103 */
+    uint16_t* value_cache;
+} xo_block;
+
+struct xo_model {
+    xh_config c;
+    xo_tensor embed, final_norm, wcls;
+    xo_block* blocks;
+    /* InferenceState, src/model.h:97-108 */
+    float *x, *xb, *xb2, *hb, *hb2, *q, *k, *v, *att, *logits;
+};
+
+static void* xcalloc(size_t n, size_t sz) { return calloc(n ? n : 1, sz); }
+
+xo_model* xo_create(const xh_config* cfg) {
+    xo_model* m = (xo_model*)xcalloc(1, sizeof(xo_model));
+    if (!m) return NULL;
+    m->c = *cfg;
+    const xh_config* c = cfg;
+    const size_t q_dim = (size_t)c->n_heads * c->head_dim, kv_dim = (size_t)c->n_kv_heads * c->head_dim;
+    m->blocks = (xo_block*)xcalloc((size_t)c->n_layers, sizeof(xo_block));
+    for (int l = 0; l < c->n_layers; l++) {
+        m->blocks[l].key_cache = (uint16_t*)xcalloc((size_t)c->max_seq_len * kv_dim, 2);
+        m->blocks[l].value_cache = (uint16_t*)xcalloc((size_t)c->max_seq_len * kv_dim, 2);
+    }
+    /* xb2 sized max(dim, q_dim): the reference sizes it [dim] and writes q_dim floats */
+    const size_t xb2n = q_dim > (size_t)c->dim ? q_dim : (size_t)c->dim;
+    m->x = (float*)xcalloc(c->dim, 4);
+    m->xb = (float*)xcalloc(c->dim, 4);
+    m->xb2 = (float*)xcalloc(xb2n, 4);
+    /* hb also receives the Wo output [dim] (src/infer.cpp:447); size it for both */
+    const size_t hbn = (size_t)c->hidden_dim > (size_t)c->dim ? (size_t)c->hidden_dim : (size_t)c->dim;
+    m->hb = (float*)xcalloc(hbn, 4);
+    m->hb2 = (float*)xcalloc(c->hidden_dim, 4);
+    m->q = (float*)xcalloc(q_dim, 4);
+    m->k = (float*)xcalloc(kv_dim, 4);
+    m->v = (float*)xcalloc(kv_dim, 4);
+    m->att = (float*)xcalloc((size_t)c->n_heads * c->max_seq_len, 4);
+    m->logits = (float*)xcalloc(c->vocab_size, 4);
+    return m;
+}
+
+void xo_destroy(xo_model* m) {
+    if (!m) return;
+    for (int l = 0; l < m->c.n_layers; l++) {
+        free(m->blocks[l].key_cache);
+        free(m->blocks[l].value_cache);
+    }
+    free(m->blocks);
+    free(m->x); free(m->xb); free(m->xb2); free(m->hb); free(m->hb2);
+    free(m->q); free(m->k); free(m->v); free(m->att); free(m->logits);
+    free(m);
+}
+
+void xo_reset(xo_model* m) {
+    const size_t kv_dim = (size_t)m->c.n_kv_heads * m->c.head_dim;
+    for (int l = 0; l < m->c.n_layers; l++) {
+        memset(m->blocks[l].key_cache, 0, (size_t)m->c.max_seq_len * kv_dim * 2);
+        memset(m->blocks[l].value_cache, 0, (size_t)m->c.max_seq_len * kv_dim * 2);
+    }
+}
+
+int xo_set_tensor(xo_model* m, int kind, int layer, int dtype, const void* data) {
+    if (kind < 0 || kind >= XH_NUM_KINDS || !data) return XH_E_INVALID;
+    xo_tensor t = {dtype, data};
+    if (kind == XH_EMBED) m->embed = t;
+    else if (kind == XH_FINAL_NORM) m->final_norm = t;
+    else if (kind == XH_WCLS) m->wcls = t;
+    else {
+        if (layer < 0 || layer >= m->c.n_layers) return XH_E_INVALID;
+        m->blocks[layer].t[kind] = t;
+    }
+    return 0;
+}
+
+const float* xo_logits(const xo_model* m) { return m->logits; }
+uint16_t* xo_key_cache(xo_model* m, int layer) { return m->blocks[layer].key_cache; }
+uint16_t* xo_value_cache(xo_model* m, int layer) { return m->blocks[layer].value_cache; }
+
+/* Model::active_bytes, src/model.cpp:12-35 */
+size_t xo_active_bytes(const xo_model* m, size_t pos) {
+    const xh_config* c = &m->c;
+    size_t bytes = 0;
+    bytes += (size_t)c->dim * dtype_bits(m->embed.dtype) / 8;
+    bytes += (size_t)c->dim * dtype_bits(m->final_norm.dtype) / 8;
+    bytes += (size_t)c->vocab_size * c->dim * dtype_bits(m->wcls.dtype) / 8;
+    for (int l = 0; l < c->n_layers; ++l) {
+        const xo_tensor* t = m->blocks[l].t;
+        bytes += (size_t)c->dim * dtype_bits(t[XH_ATTN_NORM].dtype) / 8;
+        bytes += (size_t)c->dim * dtype_bits(t[XH_FFN_NORM].dtype) / 8;
+        bytes += (size_t)c->n_heads * c->head_dim * c->dim * dtype_bits(t[XH_WQ].dtype) / 8;
+        bytes += (size_t)c->n_kv_heads * c->head_dim * c->dim * dtype_bits(t[XH_WK].dtype) / 8;
+        bytes += (size_t)c->n_kv_heads * c->head_dim * c->dim * dtype_bits(t[XH_WV].dtype) / 8;
+        bytes += (size_t)c->n_heads * c->head_dim * c->dim * dtype_bits(t[XH_WO].dtype) / 8;
+        bytes += (size_t)c->dim * c->hidden_dim * dtype_bits(t[XH_W1].dtype) / 8;
+        bytes += (size_t)c->dim * c->hidden_dim * dtype_bits(t[XH_W2].dtype) / 8;
+        bytes += (size_t)c->dim * c->hidden_dim * dtype_bits(t[XH_W3].dtype) / 8;
+        const size_t kv_len = (size_t)c->max_seq_len < pos + 1 ? (size_t)c->max_seq_len : pos + 1;
+        bytes += 2 * kv_len * c->n_kv_heads * c->head_dim * 2;
+    }
+    return bytes;
+}
+
+/* Model::_copy_embedding, src/infer.cpp:553-602 */
+static void copy_embedding(xo_model* m, const int token) {
+    for (int i = 0; i < m->c.dim; ++i) m->x[i] = xo_decode(m->embed.dtype, m->embed.data, (size_t)token * m->c.dim + i);
+}
+
+/* Block::_block_cpu, src/infer.cpp:365-496 */
+static void block_cpu(xo_model* m, const xo_block* b, const int pos, const int kv_sink, const int kv_pos,
+                      const int kv_len) {
+    const xh_config* c = &m->c;
+    const xo_tensor* t = b->t;
+    /* attention pre-norm :374-382 */
+    xo_rmsnorm(m->xb, m->x, t[XH_ATTN_NORM].data, t[XH_ATTN_NORM].dtype, c->dim, c->norm_eps);
+    const int q_dim = c->n_heads * c->head_dim;
+    const int kv_dim = c->n_kv_heads * c->head_dim;
+    /* qkv matmuls :388-390 */
+    xo_matmul(m->q, m->xb, t[XH_WQ].data, t[XH_WQ].dtype, c->dim, q_dim);
+    xo_matmul(m->k, m->xb, t[XH_WK].data, t[XH_WK].dtype, c->dim, kv_dim);
+    xo_matmul(m->v, m->xb, t[XH_WV].data, t[XH_WV].dtype, c->dim, kv_dim);
+    /* qkv clip :392-399 */
+    for (int i = 0; i < q_dim; ++i) m->q[i] = clip(m->q[i], c->qkv_clip);
+    for (int i = 0; i < kv_dim; ++i) {
+        m->k[i] = clip(m->k[i], c->qkv_clip);
+        m->v[i] = clip(m->v[i], c->qkv_clip);
+    }
+    uint16_t* kb = b->key_cache;
+    uint16_t* vb = b->value_cache;
+    /* RoPE :407-408 */
+    xo_rope(m->q, q_dim, c->head_dim, pos, c->rope_theta, c->rotary_dim);
+    xo_rope(m->k, kv_dim, c->head_dim, pos, c->rope_theta, c->rotary_dim);
+    /* kv cache write (fp32 -> fp16) :411-414 */
+    for (int i = 0; i < kv_dim; ++i) {
+        kb[(size_t)kv_pos * kv_dim + i] = xo_f32_to_f16(m->k[i]);
+        vb[(size_t)kv_pos * kv_dim + i] = xo_f32_to_f16(m->v[i]);
+    }
+    /* sink re-rotation by +1 position, fp16 round trip :421-431 */
+    for (int r = 0; r < kv_sink; r++) {
+        for (int i = 0; i < kv_dim; ++i) m->k[i] = xo_f16_to_f32(kb[(size_t)r * kv_dim + i]);
+        xo_rope(m->k, kv_dim, c->head_dim, 1, c->rope_theta, c->rotary_dim);
+        for (int i = 0; i < kv_dim; i++) kb[(size_t)r * kv_dim + i] = xo_f32_to_f16(m->k[i]);
+    }
+    /* multi-head attention :435-444 */
+    xo_mha(m->xb2, m->att, kb, vb, m->q, c->head_dim, kv_len, c->max_seq_len, c->n_heads, c->n_kv_heads);
+    /* output projection + residual :447-452 */
+    xo_matmul(m->hb, m->xb2, t[XH_WO].data, t[XH_WO].dtype, q_dim, c->dim);
+    for (int i = 0; i < c->dim; ++i) m->x[i] += m->hb[i];
+    /* ffn pre-norm :455-463 */
+    xo_rmsnorm(m->xb, m->x, t[XH_FFN_NORM].data, t[XH_FFN_NORM].dtype, c->dim, c->norm_eps);
+    /* GLU ffn :468-494 */
+    xo_matmul(m->hb, m->xb, t[XH_W1].data, t[XH_W1].dtype, c->dim, c->hidden_dim);
+    xo_matmul(m->hb2, m->xb, t[XH_W3].data, t[XH_W3].dtype, c->dim, c->hidden_dim);
+    if (c->act == XH_ACT_GELU) {
+        for (int i = 0; i < c->hidden_dim; ++i) m->hb[i] = gelu(m->hb[i]) * m->hb2[i];
+    } else {
+        for (int i = 0; i < c->hidden_dim; ++i) m->hb[i] = silu(m->hb[i]) * m->hb2[i];
+    }
+    xo_matmul(m->xb2, m->hb, t[XH_W2].data, t[XH_W2].dtype, c->hidden_dim, c->dim);
+    for (int i = 0; i < c->dim; ++i) m->x[i] += m->xb2[i];
+}
+
+/* Model::_forward_cpu, src/infer.cpp:604-638 */
+int xo_forward(xo_model* m, const int token, const int pos, const int mode) {
+    const xh_config* c = &m->c;
+    if (token < 0 || token >= c->vocab_size || pos < 0) return XH_E_INVALID;
+    if (!m->embed.data || !m->final_norm.data || !m->wcls.data) return XH_E_STATE;
+    for (int l = 0; l < c->n_layers; l++)
+        for (int k = XH_ATTN_NORM; k <= XH_W3; k++)
+            if (!m->blocks[l].t[k].data) return XH_E_STATE;
+    copy_embedding(m, token);
+    /* ring / sink bookkeeping :611-613 */
+    const int kv_sink = pos >= c->max_seq_len ? KV_SINKS : 0;
+    const int kv_pos = kv_sink + (pos - kv_sink) % (c->max_seq_len - kv_sink);
+    const int kv_len = pos >= c->max_seq_len ? c->max_seq_len : pos + 1;
+    for (int l = 0; l < c->n_layers; l++) block_cpu(m, &m->blocks[l], pos, kv_sink, kv_pos, kv_len);
+    if (mode == XH_HYDRATE_KV_CACHE) return 0; /* :620-623 */
+    xo_rmsnorm(m->x, m->x, m->final_norm.data, m->final_norm.dtype, c->dim, c->norm_eps); /* :626-634 */
+    xo_matmul(m->logits, m->x, m->wcls.data, m->wcls.dtype, c->dim, c->vocab_size);       /* :637 */
+    return 0;
+}

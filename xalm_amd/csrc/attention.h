@@ -1,0 +1,180 @@
+// attention.h — single-token GQA attention over the fp16 KV ring (split-KV "flash decoding").
+//
+// Replaces the head loop of Block::_block_cpu (jubruckne/Xalm src/infer.cpp:434-444) and
+// `attn` (src/infer.cpp:325-359) + `softmax` (:280-297):
+//   s_t = (q_h . K[t, g]) * (1/sqrtf(hd)),  t in [0, kv_len) ring slots
+//   p   = softmax(s)   (max-subtract, expf)
+//   o_h = sum_t p_t V[t, g],   g = h / (n_heads / n_kv_heads)
+// One workgroup serves one KV head and a contiguous slot range, so each K/V row is read from
+// HBM once for all q heads of its group (the CPU re-reads it per q head).  The slot range
+// length T is chosen on device from kv_len so the grid shape never changes (graph replay).
+// With more than one active split, partial (o, m, l) are merged by attn_combine_kernel.
+#pragma once
+
+#include <float.h>
+
+#include "common.h"
+
+namespace xalm {
+
+constexpr int ATTN_THREADS = 256;
+
+struct AttnArgs {
+    const float* q;          // [n_heads * HD], roped
+    const uint16_t* kc;      // [max_seq_len][kv_dim] fp16 bits
+    const uint16_t* vc;
+    int kv_dim;
+    int n_heads;
+    int nsplit;              // gridDim.y
+    float* out;              // [n_heads * HD]
+    float* part_o;           // [nsplit][n_heads][HD]
+    float* part_ml;          // [nsplit][n_heads][2]
+    const StepParams* sp;
+};
+
+// slots per split for this step: >= 16, multiple of 16, nsplit * T >= kv_len
+__device__ __host__ __forceinline__ int attn_split_len(const int kv_len, const int nsplit) {
+    int t = (kv_len + nsplit - 1) / nsplit;
+    t = (t + 15) & ~15;
+    return t < 16 ? 16 : t;
+}
+
+template <int HD, int QPK>
+__global__ __launch_bounds__(ATTN_THREADS) void attn_split_kernel(const AttnArgs a) {
+    constexpr int LPR = HD / 8;               // lanes per K/V row (16 B = 8 fp16 each)
+    constexpr int RPP = ATTN_THREADS / LPR;   // rows per pass
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    float* red = (float*)smem;                               // [4][QPK][HD]
+    float* ml = red + 4 * QPK * HD;                          // [QPK][2]
+    float* sc = ml + ((2 * QPK + 3) & ~3);                   // [QPK][T]
+
+    const int kv_len = a.sp->kv_len;
+    const int T = attn_split_len(kv_len, a.nsplit);
+    const int g = blockIdx.x, s = blockIdx.y;
+    const int t0 = s * T;
+    if (t0 >= kv_len) return;
+    const int t1 = min(kv_len, t0 + T);
+    const int n_active = (kv_len + T - 1) / T;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int sub = tid % LPR, rr = tid / LPR;
+    const float scale = 1.0f / sqrtf((float)HD);  // src/infer.cpp:338
+
+    float qv[QPK][8];
+#pragma unroll
+    for (int h = 0; h < QPK; h++) {
+        const float4* qp = (const float4*)(a.q + (size_t)(g * QPK + h) * HD + sub * 8);
+        const float4 q0 = qp[0], q1 = qp[1];
+        qv[h][0] = q0.x; qv[h][1] = q0.y; qv[h][2] = q0.z; qv[h][3] = q0.w;
+        qv[h][4] = q1.x; qv[h][5] = q1.y; qv[h][6] = q1.z; qv[h][7] = q1.w;
+    }
+    const size_t col = (size_t)g * HD + sub * 8;
+
+    // ---- scores ----
+    for (int t = t0 + rr; t < t1; t += RPP) {
+        const u32x4 kw = *(const u32x4*)(a.kc + (size_t)t * a.kv_dim + col);
+        float kf[8];
+        WDec<XH_F16>::dec(kw, kf);
+#pragma unroll
+        for (int h = 0; h < QPK; h++) {
+            float p = 0.f;
+#pragma unroll
+            for (int i = 0; i < 8; i++) p = fmaf(qv[h][i], kf[i], p);
+#pragma unroll
+            for (int o = LPR / 2; o > 0; o >>= 1) p += __shfl_xor(p, o, 64);
+            if (sub == 0) sc[h * T + (t - t0)] = p * scale;
+        }
+    }
+    __syncthreads();
+
+    // ---- softmax statistics per head (max-subtract + expf, src/infer.cpp:280-297) ----
+    const int len = t1 - t0;
+    for (int h = wid; h < QPK; h += ATTN_THREADS / 64) {
+        float m = -FLT_MAX;
+        for (int i = lane; i < len; i += 64) m = fmaxf(m, sc[h * T + i]);
+        m = wave_max(m);
+        float l = 0.f;
+        for (int i = lane; i < len; i += 64) {
+            const float e = expf(sc[h * T + i] - m);
+            sc[h * T + i] = e;
+            l += e;
+        }
+        l = wave_sum(l);
+        if (lane == 0) { ml[2 * h] = m; ml[2 * h + 1] = l; }
+    }
+    __syncthreads();
+
+    // ---- p . V ----
+    float acc[QPK][8];
+#pragma unroll
+    for (int h = 0; h < QPK; h++)
+#pragma unroll
+        for (int i = 0; i < 8; i++) acc[h][i] = 0.f;
+    for (int t = t0 + rr; t < t1; t += RPP) {
+        const u32x4 vw = *(const u32x4*)(a.vc + (size_t)t * a.kv_dim + col);
+        float vf[8];
+        WDec<XH_F16>::dec(vw, vf);
+#pragma unroll
+        for (int h = 0; h < QPK; h++) {
+            const float e = sc[h * T + (t - t0)];
+#pragma unroll
+            for (int i = 0; i < 8; i++) acc[h][i] = fmaf(e, vf[i], acc[h][i]);
+        }
+    }
+    // reduce over the row slots of this wave (lanes sharing `sub`), then over waves
+#pragma unroll
+    for (int h = 0; h < QPK; h++)
+#pragma unroll
+        for (int i = 0; i < 8; i++)
+#pragma unroll
+            for (int o = LPR; o < 64; o <<= 1) acc[h][i] += __shfl_xor(acc[h][i], o, 64);
+    if (lane < LPR) {
+#pragma unroll
+        for (int h = 0; h < QPK; h++)
+#pragma unroll
+            for (int i = 0; i < 8; i++) red[(wid * QPK + h) * HD + sub * 8 + i] = acc[h][i];
+    }
+    __syncthreads();
+    for (int idx = tid; idx < QPK * HD; idx += ATTN_THREADS) {
+        const int h = idx / HD;
+        const float o = red[idx] + red[QPK * HD + idx] + red[2 * QPK * HD + idx] + red[3 * QPK * HD + idx];
+        const int head = g * QPK + h;
+        const int d = idx - h * HD;
+        if (n_active == 1) {
+            a.out[(size_t)head * HD + d] = o / ml[2 * h + 1];
+        } else {
+            a.part_o[((size_t)s * a.n_heads + head) * HD + d] = o;
+            if (d == 0) {
+                a.part_ml[((size_t)s * a.n_heads + head) * 2] = ml[2 * h];
+                a.part_ml[((size_t)s * a.n_heads + head) * 2 + 1] = ml[2 * h + 1];
+            }
+        }
+    }
+}
+
+// merge split partials: out = sum_s e^{m_s-M} o_s / sum_s e^{m_s-M} l_s
+__global__ void attn_combine_kernel(const AttnArgs a, const int hd) {
+    const int kv_len = a.sp->kv_len;
+    const int T = attn_split_len(kv_len, a.nsplit);
+    const int n_active = (kv_len + T - 1) / T;
+    if (n_active <= 1) return;
+    const int head = blockIdx.x;
+    float M = -FLT_MAX;
+    for (int s = 0; s < n_active; s++) M = fmaxf(M, a.part_ml[((size_t)s * a.n_heads + head) * 2]);
+    for (int d = threadIdx.x; d < hd; d += blockDim.x) {
+        float num = 0.f, den = 0.f;
+        for (int s = 0; s < n_active; s++) {
+            const float* mlp = a.part_ml + ((size_t)s * a.n_heads + head) * 2;
+            const float f = expf(mlp[0] - M);
+            num = fmaf(f, a.part_o[((size_t)s * a.n_heads + head) * hd + d], num);
+            den = fmaf(f, mlp[1], den);
+        }
+        a.out[(size_t)head * hd + d] = num / den;
+    }
+}
+
+// shared-memory bytes of attn_split_kernel<HD,QPK> for a given max split length
+inline size_t attn_smem_bytes(const int hd, const int qpk, const int t_max) {
+    return sizeof(float) * (4 * qpk * hd + ((2 * qpk + 3) & ~3) + (size_t)qpk * t_max);
+}
+
+}  // namespace xalm

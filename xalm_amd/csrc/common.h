@@ -1,0 +1,166 @@
+// common.h — device-side element decode and wave/block reductions for gfx950.
+//
+// Decode semantics are the reference's (jubruckne/Xalm src/types.h), bit for bit:
+//   f16   : IEEE binary16 -> f32 (ARM float16_t promotion)
+//   bf16  : bits << 16                                   (bf16_to_f32, src/types.h:322-325)
+//   e4m3  : ((b&0x80)<<24 | (b&0x7f)<<20) * 2^120        (f8_t::to_float, src/types.h:302-314)
+//   e5m2  : ((b&0x80)<<24 | (b&0x7f)<<21) * 2^112        (same, M=2)
+//   q8    : (1.f/100.f) * (float)int8                    (Type::Q8, src/types.h:423-424)
+// The fp8 forms equal OCP e4m3fn / e5m2 for every finite code and give the reference's
+// finite values for the NaN/Inf codes (e4m3 0x7F -> 480), which the hardware converter
+// would not, so the bit form is used.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/xalm_hip.h"
+
+namespace xalm {
+
+typedef _Float16 h2_t __attribute__((ext_vector_type(2)));
+typedef float f2_t __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));  // native vector: nontemporal loads
+
+__device__ __forceinline__ float bits_f32(uint32_t u) { return __builtin_bit_cast(float, u); }
+
+// 16 bytes of weights -> E floats.  E = 16 / sizeof(element).
+template <int DT> struct WDec;
+
+template <> struct WDec<XH_F32> {
+    static constexpr int E = 4;
+    __device__ __forceinline__ static void dec(const u32x4 v, float* f) {
+        f[0] = bits_f32(v.x); f[1] = bits_f32(v.y); f[2] = bits_f32(v.z); f[3] = bits_f32(v.w);
+    }
+};
+
+template <> struct WDec<XH_F16> {
+    static constexpr int E = 8;
+    __device__ __forceinline__ static void dec(const u32x4 v, float* f) {
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const f2_t p = __builtin_convertvector(__builtin_bit_cast(h2_t, w[i]), f2_t);
+            f[2 * i] = p.x;
+            f[2 * i + 1] = p.y;
+        }
+    }
+};
+
+template <> struct WDec<XH_BF16> {
+    static constexpr int E = 8;
+    __device__ __forceinline__ static void dec(const u32x4 v, float* f) {
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            f[2 * i] = bits_f32(w[i] << 16);
+            f[2 * i + 1] = bits_f32(w[i] & 0xffff0000u);
+        }
+    }
+};
+
+template <int SHIFT, int SCALE_EXP>
+__device__ __forceinline__ void dec_f8_word(const uint32_t w, float* f) {
+    // byte k of w -> sign to bit 31, low 7 bits to the top of the f32 exponent field
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const uint32_t b = (w >> (8 * k)) & 0xffu;
+        const uint32_t u = ((b & 0x80u) << 24) | ((b & 0x7fu) << SHIFT);
+        f[k] = bits_f32(u) * __builtin_bit_cast(float, (uint32_t)((127 + SCALE_EXP) << 23));
+    }
+}
+
+template <> struct WDec<XH_F8_E4M3> {
+    static constexpr int E = 16;
+    __device__ __forceinline__ static void dec(const u32x4 v, float* f) {
+        dec_f8_word<20, 120>(v.x, f);
+        dec_f8_word<20, 120>(v.y, f + 4);
+        dec_f8_word<20, 120>(v.z, f + 8);
+        dec_f8_word<20, 120>(v.w, f + 12);
+    }
+};
+
+template <> struct WDec<XH_F8_E5M2> {
+    static constexpr int E = 16;
+    __device__ __forceinline__ static void dec(const u32x4 v, float* f) {
+        dec_f8_word<21, 112>(v.x, f);
+        dec_f8_word<21, 112>(v.y, f + 4);
+        dec_f8_word<21, 112>(v.z, f + 8);
+        dec_f8_word<21, 112>(v.w, f + 12);
+    }
+};
+
+template <> struct WDec<XH_Q8> {
+    static constexpr int E = 16;
+    __device__ __forceinline__ static void dec(const u32x4 v, float* f) {
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const int8_t q = (int8_t)((w[i] >> (8 * k)) & 0xffu);
+                f[4 * i + k] = (1.f / 100.f) * (float)q;
+            }
+    }
+};
+
+// single-element decode (embedding gather, norm weights)
+__device__ __forceinline__ float dec1(const int dtype, const void* p, const size_t i) {
+    switch (dtype) {
+        case XH_F32: return ((const float*)p)[i];
+        case XH_F16: return (float)((const _Float16*)p)[i];
+        case XH_BF16: return bits_f32((uint32_t)((const uint16_t*)p)[i] << 16);
+        case XH_F8_E4M3: {
+            const uint32_t b = ((const uint8_t*)p)[i];
+            return bits_f32(((b & 0x80u) << 24) | ((b & 0x7fu) << 20)) * 0x1p120f;
+        }
+        case XH_F8_E5M2: {
+            const uint32_t b = ((const uint8_t*)p)[i];
+            return bits_f32(((b & 0x80u) << 24) | ((b & 0x7fu) << 21)) * 0x1p112f;
+        }
+        case XH_Q8: return (1.f / 100.f) * (float)((const int8_t*)p)[i];
+        default: return __builtin_nanf("");
+    }
+}
+
+__device__ __forceinline__ uint16_t f32_to_f16_bits(const float f) {
+    return __builtin_bit_cast(uint16_t, (_Float16)f);  // v_cvt_f16_f32, round-to-nearest-even
+}
+__device__ __forceinline__ float f16_bits_to_f32(const uint16_t h) {
+    return (float)__builtin_bit_cast(_Float16, h);
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+// Per-token dynamic scalars, read by every kernel of a captured graph.
+// kv_sink / kv_pos / kv_len follow src/infer.cpp:611-613.
+struct StepParams {
+    int token;
+    int pos;
+    int kv_sink;
+    int kv_pos;
+    int kv_len;
+    int step;      // device decode loop: index into the token output buffer
+    int pos_next;  // device decode loop: position of the next forward
+    int max_seq_len;
+};
+
+__device__ __forceinline__ void step_positions(StepParams* sp, const int pos) {
+    const int msl = sp->max_seq_len;
+    const int kv_sink = pos >= msl ? 2 : 0;  // KV_SINKS, src/model.h:10
+    sp->pos = pos;
+    sp->kv_sink = kv_sink;
+    sp->kv_pos = kv_sink + (pos - kv_sink) % (msl - kv_sink);
+    sp->kv_len = pos >= msl ? msl : pos + 1;
+}
+
+}  // namespace xalm

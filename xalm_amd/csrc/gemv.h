@@ -1,0 +1,286 @@
+// gemv.h — batch-1 weight-streaming matvec for gfx950 with fused prologues/epilogues.
+//
+// Replaces `matmul<TX,TW>` (jubruckne/Xalm src/infer.cpp:104-135, dispatch :185-216) and
+// the elementwise ops around each call site in Block::_block_cpu (src/infer.cpp:365-496):
+//   prologue  PRO_RMSNORM : rmsnorm(xb, x, w) (src/infer.cpp:224-236) recomputed per block
+//   epilogue  EPI_QKV     : qkv clip (:392-399), rope (:305-322, :407-408), fp16 KV write (:410-414)
+//             EPI_GLU     : hb = act(W1 x) * (W3 x) (:468-488), W1/W3 rows interleaved
+//             EPI_RESID   : x += W x (:447-452, :490-494)
+//             EPI_STORE   : y = W x (logits, :637)
+//
+// HBM layout: W row-major [rows][n] exactly as the .xalm tensor (HF [out,in]).  One wave
+// owns ROWS consecutive rows; lane l streams 16-byte chunks l, l+64, l+128, ... of each row
+// (1 KiB per wave-instruction per row, fully coalesced) with non-temporal loads (weights are
+// read once per token).  The activation vector is staged once per workgroup in LDS in a
+// lane-permuted layout so every lane reads its matching x values with conflict-free
+// ds_read_b128.  Dot products reduce across the wave with cross-lane shuffles; there is no
+// MFMA: batch-1 matvec is HBM-bound at ~1 FLOP per weight byte.
+#pragma once
+
+#include "common.h"
+
+namespace xalm {
+
+enum { PRO_PLAIN = 0, PRO_RMSNORM = 1 };
+enum { EPI_STORE = 0, EPI_RESID = 1, EPI_QKV = 2, EPI_GLU = 3 };
+
+constexpr int GEMV_THREADS = 256;
+constexpr int GEMV_WAVES = GEMV_THREADS / 64;
+constexpr int LDS_HEAD_BYTES = 64;  // block-reduction scratch in front of the x image
+
+struct GemvArgs {
+    const void* w;        // [rows][n]
+    size_t row_bytes;     // n * sizeof(element)
+    int n;                // input length
+    int rows;             // output rows
+    const float* x;       // input [n], fp32
+    const void* norm_w;   // PRO_RMSNORM weight [n] (F32 or BF16)
+    int norm_dtype;
+    float eps;
+    float* out;           // EPI_STORE / EPI_RESID: [rows];  EPI_GLU: [rows/2]
+    // EPI_QKV
+    float* q;             // [q_dim]
+    uint16_t* kcache;     // this layer's K ring [max_seq_len][kv_dim] (fp16 bits)
+    uint16_t* vcache;
+    int q_dim;
+    int kv_dim;
+    int head_dim;
+    const float* rope_freq;  // [head_dim/2]: 1/powf(theta, j/rotary_dim) or 0 (host libm)
+    const float* sink_cos;   // [head_dim/2]: cosf(freq) (rope at pos=1, host libm)
+    const float* sink_sin;
+    float qkv_clip;
+    int act;
+    const StepParams* sp;
+};
+
+__device__ __forceinline__ float clipf(const float x, const float v) { return x < -v ? -v : (x > v ? v : x); }
+
+// silu / gelu exactly as src/infer.cpp:299-301
+__device__ __forceinline__ float act_fn(const int act, const float x) {
+    if (act == XH_ACT_SILU) return x / (1.0f + expf(-x));
+    return 0.5f * x * (1.0f + tanhf(0.797885f * (x + 0.044715f * x * x * x)));
+}
+
+// One rope rotation of the adjacent pair (v0, v1) at element index i (src/infer.cpp:308-321).
+__device__ __forceinline__ void rope_pair(float& v0, float& v1, const int i, const int head_dim, const int pos,
+                                          const float* freq_tab) {
+    const int j_head = i % head_dim;
+    const float freq = freq_tab[j_head >> 1];
+    const float val = (float)pos * freq;
+    const float fcr = cosf(val);
+    const float fci = sinf(val);
+    const float a = v0, b = v1;
+    v0 = a * fcr - b * fci;
+    v1 = a * fci + b * fcr;
+}
+
+// Sum of squares of x[0..n) -> rms scale 1/sqrtf(ss/n + eps), identical in every block
+// (fixed per-thread stride order, fixed shuffle tree, fixed wave order).
+__device__ __forceinline__ float block_rms_scale(const float* x, const int n, const float eps, float* red) {
+    const int tid = threadIdx.x;
+    const float4* x4 = (const float4*)x;
+    float ss = 0.f;
+    for (int i = tid; i < (n >> 2); i += GEMV_THREADS) {
+        const float4 v = x4[i];
+        ss += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+    }
+    ss = wave_sum(ss);
+    if ((tid & 63) == 0) red[tid >> 6] = ss;
+    __syncthreads();
+    float tot = 0.f;
+#pragma unroll
+    for (int w = 0; w < GEMV_WAVES; w++) tot += red[w];
+    const float rms = sqrtf(tot / (float)n + eps);
+    return 1.0f / rms;
+}
+
+__device__ __forceinline__ float4 load_norm4(const void* w, const int dtype, const int i4) {
+    if (dtype == XH_BF16) {
+        const uint2 u = ((const uint2*)w)[i4];
+        return make_float4(bits_f32(u.x << 16), bits_f32(u.x & 0xffff0000u), bits_f32(u.y << 16),
+                           bits_f32(u.y & 0xffff0000u));
+    }
+    return ((const float4*)w)[i4];
+}
+
+// x (optionally rms-normalised and weighted) -> LDS image xs4, permuted so that lane l at
+// chunk `it` finds the E/4 float4 it multiplies at xs4[(it*E/4 + q)*64 + l].
+template <int E, int PRO>
+__device__ __forceinline__ void stage_x(const GemvArgs& a, float4* xs4, float* red) {
+    const int n = a.n;
+    float scale = 1.f;
+    if (PRO == PRO_RMSNORM) scale = block_rms_scale(a.x, n, a.eps, red);
+    const float4* x4 = (const float4*)a.x;
+    for (int i = threadIdx.x; i < (n >> 2); i += GEMV_THREADS) {
+        float4 v = x4[i];
+        if (PRO == PRO_RMSNORM) {
+            const float4 w = load_norm4(a.norm_w, a.norm_dtype, i);
+            v.x = v.x * scale * w.x;  // x[i] * scale * weight[i], src/infer.cpp:234
+            v.y = v.y * scale * w.y;
+            v.z = v.z * scale * w.z;
+            v.w = v.w * scale * w.w;
+        }
+        const int c = i << 2;
+        const int it = c / (64 * E);
+        const int rem = c - it * 64 * E;
+        const int l = rem / E;
+        const int qd = (rem - l * E) >> 2;
+        xs4[(it * (E / 4) + qd) * 64 + l] = v;
+    }
+}
+
+// StreamingLLM sink re-rotation (src/infer.cpp:421-431): K[r] = f16(rope(f32(K[r]), pos=1)).
+__device__ __forceinline__ void rotate_sinks(const GemvArgs& a, const int kv_sink) {
+    for (int r = 0; r < kv_sink; r++) {
+        uint16_t* krow = a.kcache + (size_t)r * a.kv_dim;
+        for (int p = threadIdx.x; p < (a.kv_dim >> 1); p += GEMV_THREADS) {
+            const int i = p << 1;
+            const int jh = (i % a.head_dim) >> 1;
+            const float k0 = f16_bits_to_f32(krow[i]), k1 = f16_bits_to_f32(krow[i + 1]);
+            const float fcr = a.sink_cos[jh], fci = a.sink_sin[jh];
+            krow[i] = f32_to_f16_bits(k0 * fcr - k1 * fci);
+            krow[i + 1] = f32_to_f16_bits(k0 * fci + k1 * fcr);
+        }
+    }
+}
+
+template <int EPI, int ROWS>
+__device__ __forceinline__ void gemv_epilogue(const GemvArgs& a, const int row0, const float* acc) {
+    if (EPI == EPI_STORE) {
+#pragma unroll
+        for (int r = 0; r < ROWS; r++)
+            if (row0 + r < a.rows) a.out[row0 + r] = acc[r];
+    } else if (EPI == EPI_RESID) {
+#pragma unroll
+        for (int r = 0; r < ROWS; r++)
+            if (row0 + r < a.rows) a.out[row0 + r] += acc[r];
+    } else if (EPI == EPI_GLU) {
+#pragma unroll
+        for (int p = 0; p < ROWS; p += 2) a.out[(row0 + p) >> 1] = act_fn(a.act, acc[p]) * acc[p + 1];
+    } else {  // EPI_QKV
+        const int pos = a.sp->pos;
+        const int kv_pos = a.sp->kv_pos;
+#pragma unroll
+        for (int p = 0; p < ROWS; p += 2) {
+            const int row = row0 + p;
+            float v0 = clipf(acc[p], a.qkv_clip), v1 = clipf(acc[p + 1], a.qkv_clip);
+            if (row < a.q_dim) {
+                rope_pair(v0, v1, row, a.head_dim, pos, a.rope_freq);
+                a.q[row] = v0;
+                a.q[row + 1] = v1;
+            } else if (row < a.q_dim + a.kv_dim) {
+                const int kr = row - a.q_dim;
+                rope_pair(v0, v1, kr, a.head_dim, pos, a.rope_freq);
+                uint16_t* dst = a.kcache + (size_t)kv_pos * a.kv_dim + kr;
+                dst[0] = f32_to_f16_bits(v0);
+                dst[1] = f32_to_f16_bits(v1);
+            } else {
+                const int vr = row - a.q_dim - a.kv_dim;
+                uint16_t* dst = a.vcache + (size_t)kv_pos * a.kv_dim + vr;
+                dst[0] = f32_to_f16_bits(v0);
+                dst[1] = f32_to_f16_bits(v1);
+            }
+        }
+    }
+}
+
+template <int DT, int ROWS, int U>
+__device__ __forceinline__ void gemv_chunk(const char* wrow, const size_t row_bytes, const float4* xs4, const int it,
+                                           const int lane, float* acc) {
+    constexpr int E = WDec<DT>::E;
+    constexpr int QN = E / 4;
+    u32x4 wv[U][ROWS];
+#pragma unroll
+    for (int u = 0; u < U; u++)
+#pragma unroll
+        for (int r = 0; r < ROWS; r++)
+            wv[u][r] = __builtin_nontemporal_load((const u32x4*)(wrow + (size_t)r * row_bytes + (size_t)(it + u) * 1024));
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        float4 xv[QN];
+#pragma unroll
+        for (int qd = 0; qd < QN; qd++) xv[qd] = xs4[((it + u) * QN + qd) * 64 + lane];
+#pragma unroll
+        for (int r = 0; r < ROWS; r++) {
+            float f[E];
+            WDec<DT>::dec(wv[u][r], f);
+            float s = acc[r];
+#pragma unroll
+            for (int qd = 0; qd < QN; qd++) {
+                s = fmaf(f[4 * qd + 0], xv[qd].x, s);
+                s = fmaf(f[4 * qd + 1], xv[qd].y, s);
+                s = fmaf(f[4 * qd + 2], xv[qd].z, s);
+                s = fmaf(f[4 * qd + 3], xv[qd].w, s);
+            }
+            acc[r] = s;
+        }
+    }
+}
+
+template <int DT, int PRO, int EPI, int ROWS, int U>
+__global__ __launch_bounds__(GEMV_THREADS) void gemv_kernel(const GemvArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    float* red = (float*)smem;
+    float4* xs4 = (float4*)(smem + LDS_HEAD_BYTES);
+    constexpr int E = WDec<DT>::E;
+    const int lane = threadIdx.x & 63;
+    const int wid = threadIdx.x >> 6;
+
+    stage_x<E, PRO>(a, xs4, red);
+    if (EPI == EPI_QKV && blockIdx.x == 0) rotate_sinks(a, a.sp->kv_sink);
+    __syncthreads();
+
+    const int n = a.n;
+    const int n_full = n / (64 * E);
+    const int n_it = (n + 64 * E - 1) / (64 * E);
+    const int n_groups = (a.rows + ROWS - 1) / ROWS;
+    const int total_waves = gridDim.x * GEMV_WAVES;
+    for (int g = blockIdx.x * GEMV_WAVES + wid; g < n_groups; g += total_waves) {
+        const int row0 = g * ROWS;
+        // rows past the end (odd vocab) re-read the last row and are never stored
+        const int rmax = a.rows - 1;
+        const size_t rb = a.row_bytes;
+        const char* wrow = (const char*)a.w + (size_t)(row0 < rmax ? row0 : rmax) * rb + lane * 16;
+        const size_t rstride = (row0 + ROWS - 1 <= rmax) ? rb : 0;
+        float acc[ROWS];
+#pragma unroll
+        for (int r = 0; r < ROWS; r++) acc[r] = 0.f;
+        int it = 0;
+        for (; it + U <= n_full; it += U) gemv_chunk<DT, ROWS, U>(wrow, rstride, xs4, it, lane, acc);
+        for (; it < n_it; it++)
+            if ((it * 64 + lane) * E < n) gemv_chunk<DT, ROWS, 1>(wrow, rstride, xs4, it, lane, acc);
+#pragma unroll
+        for (int r = 0; r < ROWS; r++) acc[r] = wave_sum(acc[r]);
+        if (lane == 0) gemv_epilogue<EPI, ROWS>(a, row0, acc);
+    }
+}
+
+// rmsnorm as a standalone op (xh_op_rmsnorm), same reduction as the fused prologue.
+__global__ __launch_bounds__(GEMV_THREADS) void rmsnorm_kernel(float* o, const float* x, const void* w, int dtype,
+                                                                 int n, float eps) {
+    __shared__ float red[GEMV_WAVES];
+    const float scale = block_rms_scale(x, n, eps, red);
+    for (int i = threadIdx.x; i < (n >> 2); i += GEMV_THREADS) {
+        const float4 v = ((const float4*)x)[i];
+        const float4 wv = load_norm4(w, dtype, i);
+        ((float4*)o)[i] = make_float4(v.x * scale * wv.x, v.y * scale * wv.y, v.z * scale * wv.z, v.w * scale * wv.w);
+    }
+}
+
+// rope as a standalone op (xh_op_rope), same device function as the QKV epilogue.
+__global__ void rope_kernel(float* vec, int d, int head_dim, int pos, const float* freq) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (2 * p + 1 >= d + 1) return;
+    float v0 = vec[2 * p], v1 = vec[2 * p + 1];
+    rope_pair(v0, v1, 2 * p, head_dim, pos, freq);
+    vec[2 * p] = v0;
+    vec[2 * p + 1] = v1;
+}
+
+// Model::_copy_embedding (src/infer.cpp:553-602): x = dec(embed[token, :])
+__global__ void embed_kernel(const void* emb, int dtype, int dim, float* x, const StepParams* sp) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < dim) x[i] = dec1(dtype, emb, (size_t)sp->token * dim + i);
+}
+
+}  // namespace xalm

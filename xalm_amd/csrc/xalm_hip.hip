@@ -1,0 +1,942 @@
+// xalm_hip.hip — device context, weight upload, per-token graph and the C ABI (include/xalm_hip.h).
+//
+// Replaces the device branch under Xalm's `-d` switch: Model::forward -> _forward_cpu
+// (jubruckne/Xalm src/model.cpp:120-122, src/infer.cpp:604-638) and the host weight/KV
+// ownership of Model::from_xalm (src/model.cpp:48-118).
+//
+// Per token the stream runs (all launches captured once into a hipGraph and replayed; the
+// token/position scalars live in device memory, StepParams):
+//   embed_kernel                                    x = embed[token]
+//   per layer:
+//     gemv<PRO_RMSNORM, EPI_QKV>    [Wq;Wk;Wv] (one fused matrix) + rmsnorm + clip + rope +
+//                                   fp16 K/V ring write + sink re-rotation
+//     attn_split_kernel / attn_combine_kernel      GQA attention over the ring
+//     gemv<PRO_PLAIN, EPI_RESID>    Wo, x += .
+//     gemv<PRO_RMSNORM, EPI_GLU>    [W1;W3] rows interleaved + rmsnorm + silu(g)*u
+//     gemv<PRO_PLAIN, EPI_RESID>    W2, x += .
+//   gemv<PRO_RMSNORM, EPI_STORE>    final rmsnorm + lm_head -> logits   (OUTPUT_LOGITS only)
+#include <hip/hip_runtime.h>
+
+#include <cfloat>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/xalm_synth.h"
+#include "attention.h"
+#include "gemv.h"
+
+using namespace xalm;
+
+namespace {
+
+thread_local std::string g_create_error;
+
+size_t dtype_size(int dt) {
+    switch (dt) {
+        case XH_F32: return 4;
+        case XH_F16: case XH_BF16: return 2;
+        case XH_F8_E4M3: case XH_F8_E5M2: case XH_Q8: case XH_U8: return 1;
+        default: return 0;
+    }
+}
+bool matrix_dtype_ok(int dt) {
+    return dt == XH_F32 || dt == XH_F16 || dt == XH_BF16 || dt == XH_F8_E4M3 || dt == XH_F8_E5M2 || dt == XH_Q8;
+}
+int elems_per_16b(int dt) { return 16 / (int)dtype_size(dt); }
+
+constexpr int ROWS = 2;  // rows per wave (even: rope pairs, gate/up pairs)
+constexpr int UNROLL = 4;
+
+struct LayerW {
+    void* wqkv = nullptr; int qkv_dt = 0; unsigned qkv_have = 0;  // bit0 q, bit1 k, bit2 v
+    void* w13 = nullptr; int w13_dt = 0; unsigned w13_have = 0;   // bit0 w1, bit1 w3
+    void* wo = nullptr; int wo_dt = 0;
+    void* w2 = nullptr; int w2_dt = 0;
+    void* attn_norm = nullptr; int an_dt = 0;
+    void* ffn_norm = nullptr; int fn_dt = 0;
+};
+
+}  // namespace
+
+struct xh_ctx {
+    xh_config c{};
+    int dev = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+    std::vector<LayerW> L;
+    void* embed = nullptr; int embed_dt = 0;
+    void* final_norm = nullptr; int final_norm_dt = 0;
+    void* wcls = nullptr; int wcls_dt = 0;
+    int q_dim = 0, kv_dim = 0, qpk = 0;
+    uint16_t* kv = nullptr;  // [n_layers][2][max_seq_len][kv_dim]
+    float *x = nullptr, *q = nullptr, *attn_out = nullptr, *hb = nullptr, *logits = nullptr;
+    float *part_o = nullptr, *part_ml = nullptr;
+    float *rope_freq = nullptr, *sink_cos = nullptr, *sink_sin = nullptr;
+    StepParams* sp = nullptr;       // device
+    StepParams* sp_host = nullptr;  // pinned
+    int* dec_tokens = nullptr;      // device, decode loop output
+    int dec_cap = 0;
+    int nsplit = 1, t_max = 16;
+    bool use_graphs = true;
+    hipGraphExec_t g_logits = nullptr, g_hydrate = nullptr, g_decode = nullptr;
+    int max_gemv_blocks = 1024;
+
+    uint16_t* kcache(int l) { return kv + (size_t)l * 2 * c.max_seq_len * kv_dim; }
+    uint16_t* vcache(int l) { return kcache(l) + (size_t)c.max_seq_len * kv_dim; }
+};
+
+namespace {
+
+int set_err(xh_ctx* ctx, int code, const char* fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    if (ctx) ctx->err = buf; else g_create_error = buf;
+    return code;
+}
+
+#define HIP_TRY(ctx, expr)                                                                     \
+    do {                                                                                       \
+        hipError_t _e = (expr);                                                                \
+        if (_e != hipSuccess)                                                                  \
+            return set_err((ctx), XH_E_HIP, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(_e), \
+                           __FILE__, __LINE__);                                                \
+    } while (0)
+
+// ---------------------------------------------------------------------------------------
+// gemv launch dispatch
+// ---------------------------------------------------------------------------------------
+template <int DT, int PRO, int EPI>
+void launch_gemv_t(const GemvArgs& a, hipStream_t s, int max_blocks) {
+    constexpr int E = WDec<DT>::E;
+    const int n_it = (a.n + 64 * E - 1) / (64 * E);
+    const size_t smem = LDS_HEAD_BYTES + (size_t)n_it * 64 * E * sizeof(float);
+    const int n_groups = (a.rows + ROWS - 1) / ROWS;
+    int blocks = (n_groups + GEMV_WAVES - 1) / GEMV_WAVES;
+    if (blocks > max_blocks) blocks = max_blocks;
+    auto k = gemv_kernel<DT, PRO, EPI, ROWS, UNROLL>;
+    if (smem > 64 * 1024) {
+        static bool done = false;
+        if (!done) {
+            hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            done = true;
+        }
+    }
+    hipLaunchKernelGGL(k, dim3(blocks), dim3(GEMV_THREADS), smem, s, a);
+}
+
+template <int PRO, int EPI>
+bool launch_gemv(int dt, const GemvArgs& a, hipStream_t s, int max_blocks) {
+    switch (dt) {
+        case XH_F32: launch_gemv_t<XH_F32, PRO, EPI>(a, s, max_blocks); return true;
+        case XH_F16: launch_gemv_t<XH_F16, PRO, EPI>(a, s, max_blocks); return true;
+        case XH_BF16: launch_gemv_t<XH_BF16, PRO, EPI>(a, s, max_blocks); return true;
+        case XH_F8_E4M3: launch_gemv_t<XH_F8_E4M3, PRO, EPI>(a, s, max_blocks); return true;
+        case XH_F8_E5M2: launch_gemv_t<XH_F8_E5M2, PRO, EPI>(a, s, max_blocks); return true;
+        case XH_Q8: launch_gemv_t<XH_Q8, PRO, EPI>(a, s, max_blocks); return true;
+        default: return false;
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// attention launch dispatch
+// ---------------------------------------------------------------------------------------
+template <int HD, int QPK>
+void launch_attn_t(const AttnArgs& a, int n_kv_heads, int t_max, hipStream_t s) {
+    const size_t smem = attn_smem_bytes(HD, QPK, t_max);
+    auto k = attn_split_kernel<HD, QPK>;
+    if (smem > 64 * 1024) {
+        static bool done = false;
+        if (!done) {
+            hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            done = true;
+        }
+    }
+    hipLaunchKernelGGL(k, dim3(n_kv_heads, a.nsplit), dim3(ATTN_THREADS), smem, s, a);
+}
+
+template <int HD>
+bool launch_attn_hd(const AttnArgs& a, int qpk, int n_kv_heads, int t_max, hipStream_t s) {
+    switch (qpk) {
+        case 1: launch_attn_t<HD, 1>(a, n_kv_heads, t_max, s); return true;
+        case 2: launch_attn_t<HD, 2>(a, n_kv_heads, t_max, s); return true;
+        case 4: launch_attn_t<HD, 4>(a, n_kv_heads, t_max, s); return true;
+        case 8: launch_attn_t<HD, 8>(a, n_kv_heads, t_max, s); return true;
+        default: return false;
+    }
+}
+
+bool launch_attn(const AttnArgs& a, int hd, int qpk, int n_kv_heads, int t_max, hipStream_t s) {
+    bool ok = false;
+    switch (hd) {
+        case 16: ok = launch_attn_hd<16>(a, qpk, n_kv_heads, t_max, s); break;
+        case 32: ok = launch_attn_hd<32>(a, qpk, n_kv_heads, t_max, s); break;
+        case 64: ok = launch_attn_hd<64>(a, qpk, n_kv_heads, t_max, s); break;
+        case 128: ok = launch_attn_hd<128>(a, qpk, n_kv_heads, t_max, s); break;
+        case 256: ok = launch_attn_hd<256>(a, qpk, n_kv_heads, t_max, s); break;
+        default: return false;
+    }
+    if (ok && a.nsplit > 1) {
+        const int thr = hd < 64 ? 64 : hd;
+        hipLaunchKernelGGL(attn_combine_kernel, dim3(a.n_heads), dim3(thr), 0, s, a, hd);
+    }
+    return ok;
+}
+
+int attn_nsplit(int n_kv_heads, int max_seq_len) {
+    int ns = 512 / n_kv_heads;
+    const int cap = (max_seq_len + 15) / 16;
+    if (ns > cap) ns = cap;
+    return ns < 1 ? 1 : ns;
+}
+
+// ---------------------------------------------------------------------------------------
+// the per-token step, enqueued on a stream (eager or under graph capture)
+// ---------------------------------------------------------------------------------------
+GemvArgs qkv_args(xh_ctx* ctx, int l) {
+    const LayerW& w = ctx->L[l];
+    GemvArgs a{};
+    a.w = w.wqkv; a.row_bytes = (size_t)ctx->c.dim * dtype_size(w.qkv_dt);
+    a.n = ctx->c.dim; a.rows = ctx->q_dim + 2 * ctx->kv_dim; a.x = ctx->x;
+    a.norm_w = w.attn_norm; a.norm_dtype = w.an_dt; a.eps = ctx->c.norm_eps;
+    a.q = ctx->q; a.kcache = ctx->kcache(l); a.vcache = ctx->vcache(l);
+    a.q_dim = ctx->q_dim; a.kv_dim = ctx->kv_dim; a.head_dim = ctx->c.head_dim;
+    a.rope_freq = ctx->rope_freq; a.sink_cos = ctx->sink_cos; a.sink_sin = ctx->sink_sin;
+    a.qkv_clip = ctx->c.qkv_clip; a.sp = ctx->sp;
+    return a;
+}
+GemvArgs wo_args(xh_ctx* ctx, int l) {
+    const LayerW& w = ctx->L[l];
+    GemvArgs a{};
+    a.w = w.wo; a.row_bytes = (size_t)ctx->q_dim * dtype_size(w.wo_dt);
+    a.n = ctx->q_dim; a.rows = ctx->c.dim; a.x = ctx->attn_out; a.out = ctx->x; a.sp = ctx->sp;
+    return a;
+}
+GemvArgs w13_args(xh_ctx* ctx, int l) {
+    const LayerW& w = ctx->L[l];
+    GemvArgs a{};
+    a.w = w.w13; a.row_bytes = (size_t)ctx->c.dim * dtype_size(w.w13_dt);
+    a.n = ctx->c.dim; a.rows = 2 * ctx->c.hidden_dim; a.x = ctx->x;
+    a.norm_w = w.ffn_norm; a.norm_dtype = w.fn_dt; a.eps = ctx->c.norm_eps;
+    a.out = ctx->hb; a.act = ctx->c.act; a.sp = ctx->sp;
+    return a;
+}
+GemvArgs w2_args(xh_ctx* ctx, int l) {
+    const LayerW& w = ctx->L[l];
+    GemvArgs a{};
+    a.w = w.w2; a.row_bytes = (size_t)ctx->c.hidden_dim * dtype_size(w.w2_dt);
+    a.n = ctx->c.hidden_dim; a.rows = ctx->c.dim; a.x = ctx->hb; a.out = ctx->x; a.sp = ctx->sp;
+    return a;
+}
+GemvArgs cls_args(xh_ctx* ctx) {
+    GemvArgs a{};
+    a.w = ctx->wcls; a.row_bytes = (size_t)ctx->c.dim * dtype_size(ctx->wcls_dt);
+    a.n = ctx->c.dim; a.rows = ctx->c.vocab_size; a.x = ctx->x;
+    a.norm_w = ctx->final_norm; a.norm_dtype = ctx->final_norm_dt; a.eps = ctx->c.norm_eps;
+    a.out = ctx->logits; a.sp = ctx->sp;
+    return a;
+}
+AttnArgs attn_args(xh_ctx* ctx, int l) {
+    AttnArgs a{};
+    a.q = ctx->q; a.kc = ctx->kcache(l); a.vc = ctx->vcache(l); a.kv_dim = ctx->kv_dim;
+    a.n_heads = ctx->c.n_heads; a.nsplit = ctx->nsplit; a.out = ctx->attn_out;
+    a.part_o = ctx->part_o; a.part_ml = ctx->part_ml; a.sp = ctx->sp;
+    return a;
+}
+
+__global__ void argmax_advance_kernel(const float* logits, int vocab, StepParams* sp, int* tokens, int cap) {
+    // Sampler::sample_argmax (src/sampler.cpp:19-30): max starts at FLT_MIN, strict '>',
+    // so the first index of the maximum wins and all-tiny logits give token 0.
+    __shared__ float bv[1024];
+    __shared__ int bi[1024];
+    const int tid = threadIdx.x;
+    float best = FLT_MIN;
+    int idx = 0;
+    for (int i = tid; i < vocab; i += blockDim.x)
+        if (logits[i] > best) { best = logits[i]; idx = i; }
+    bv[tid] = best;
+    bi[tid] = idx;
+    __syncthreads();
+    for (int o = blockDim.x / 2; o > 0; o >>= 1) {
+        if (tid < o) {
+            const float v2 = bv[tid + o];
+            const int i2 = bi[tid + o];
+            if (v2 > bv[tid] || (v2 == bv[tid] && i2 < bi[tid])) { bv[tid] = v2; bi[tid] = i2; }
+        }
+        __syncthreads();
+    }
+    if (tid == 0) {
+        const int tok = bi[0];
+        if (sp->step < cap) tokens[sp->step] = tok;
+        sp->step += 1;
+        sp->token = tok;
+        step_positions(sp, sp->pos_next);
+        sp->pos_next += 1;
+    }
+}
+
+int enqueue_step(xh_ctx* ctx, hipStream_t s, bool with_logits) {
+    const xh_config& c = ctx->c;
+    const int mb = ctx->max_gemv_blocks;
+    hipLaunchKernelGGL(embed_kernel, dim3((c.dim + 255) / 256), dim3(256), 0, s, (const void*)ctx->embed,
+                       ctx->embed_dt, c.dim, ctx->x, (const StepParams*)ctx->sp);
+    for (int l = 0; l < c.n_layers; l++) {
+        const LayerW& w = ctx->L[l];
+        if (!launch_gemv<PRO_RMSNORM, EPI_QKV>(w.qkv_dt, qkv_args(ctx, l), s, mb))
+            return set_err(ctx, XH_E_INVALID, "layer %d: unsupported qkv dtype %d", l, w.qkv_dt);
+        if (!launch_attn(attn_args(ctx, l), c.head_dim, ctx->qpk, c.n_kv_heads, ctx->t_max, s))
+            return set_err(ctx, XH_E_INVALID, "unsupported head_dim %d / q-per-kv %d", c.head_dim, ctx->qpk);
+        if (!launch_gemv<PRO_PLAIN, EPI_RESID>(w.wo_dt, wo_args(ctx, l), s, mb))
+            return set_err(ctx, XH_E_INVALID, "layer %d: unsupported wo dtype", l);
+        if (!launch_gemv<PRO_RMSNORM, EPI_GLU>(w.w13_dt, w13_args(ctx, l), s, mb))
+            return set_err(ctx, XH_E_INVALID, "layer %d: unsupported w1/w3 dtype", l);
+        if (!launch_gemv<PRO_PLAIN, EPI_RESID>(w.w2_dt, w2_args(ctx, l), s, mb))
+            return set_err(ctx, XH_E_INVALID, "layer %d: unsupported w2 dtype", l);
+    }
+    if (with_logits) {
+        if (!launch_gemv<PRO_RMSNORM, EPI_STORE>(ctx->wcls_dt, cls_args(ctx), s, mb))
+            return set_err(ctx, XH_E_INVALID, "unsupported wcls dtype");
+    }
+    HIP_TRY(ctx, hipGetLastError());
+    return 0;
+}
+
+int check_ready(xh_ctx* ctx) {
+    if (!ctx->embed) return set_err(ctx, XH_E_STATE, "embed.weight not uploaded");
+    if (!ctx->final_norm) return set_err(ctx, XH_E_STATE, "output.norm.weight not uploaded");
+    if (!ctx->wcls) {
+        if (ctx->c.tie_word_embeddings) { ctx->wcls = ctx->embed; ctx->wcls_dt = ctx->embed_dt; }
+        else return set_err(ctx, XH_E_STATE, "output.weight not uploaded");
+    }
+    for (int l = 0; l < ctx->c.n_layers; l++) {
+        const LayerW& w = ctx->L[l];
+        if (w.qkv_have != 7 || w.w13_have != 3 || !w.wo || !w.w2 || !w.attn_norm || !w.ffn_norm)
+            return set_err(ctx, XH_E_STATE, "layer %d: weights incomplete", l);
+    }
+    return 0;
+}
+
+void drop_graphs(xh_ctx* ctx) {
+    if (ctx->g_logits) hipGraphExecDestroy(ctx->g_logits);
+    if (ctx->g_hydrate) hipGraphExecDestroy(ctx->g_hydrate);
+    if (ctx->g_decode) hipGraphExecDestroy(ctx->g_decode);
+    ctx->g_logits = ctx->g_hydrate = ctx->g_decode = nullptr;
+}
+
+int capture(xh_ctx* ctx, int kind, hipGraphExec_t* out) {
+    hipGraph_t g = nullptr;
+    HIP_TRY(ctx, hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal));
+    int rc = 0;
+    if (kind == 2) {
+        hipLaunchKernelGGL(argmax_advance_kernel, dim3(1), dim3(1024), 0, ctx->stream, (const float*)ctx->logits,
+                           ctx->c.vocab_size, ctx->sp, ctx->dec_tokens, ctx->dec_cap);
+    }
+    rc = enqueue_step(ctx, ctx->stream, kind != 1);
+    hipError_t e = hipStreamEndCapture(ctx->stream, &g);
+    if (rc) { if (g) hipGraphDestroy(g); return rc; }
+    if (e != hipSuccess) return set_err(ctx, XH_E_HIP, "graph capture failed: %s", hipGetErrorString(e));
+    e = hipGraphInstantiate(out, g, nullptr, nullptr, 0);
+    hipGraphDestroy(g);
+    if (e != hipSuccess) return set_err(ctx, XH_E_HIP, "graph instantiate failed: %s", hipGetErrorString(e));
+    return 0;
+}
+
+int run_step(xh_ctx* ctx, bool with_logits) {
+    if (!ctx->use_graphs) return enqueue_step(ctx, ctx->stream, with_logits);
+    hipGraphExec_t* ge = with_logits ? &ctx->g_logits : &ctx->g_hydrate;
+    if (!*ge) {
+        int rc = capture(ctx, with_logits ? 0 : 1, ge);
+        if (rc) return rc;
+    }
+    HIP_TRY(ctx, hipGraphLaunch(*ge, ctx->stream));
+    return 0;
+}
+
+int host_step_params(xh_ctx* ctx, int token, int pos) {
+    StepParams* h = ctx->sp_host;
+    const int msl = ctx->c.max_seq_len;
+    h->token = token;
+    h->pos = pos;
+    h->kv_sink = pos >= msl ? 2 : 0;
+    h->kv_pos = h->kv_sink + (pos - h->kv_sink) % (msl - h->kv_sink);
+    h->kv_len = pos >= msl ? msl : pos + 1;
+    h->step = 0;
+    h->pos_next = pos + 1;
+    h->max_seq_len = msl;
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->sp, h, sizeof(StepParams), hipMemcpyHostToDevice, ctx->stream));
+    return 0;
+}
+
+template <typename T>
+int dmalloc(xh_ctx* ctx, T** p, size_t n) {
+    HIP_TRY(ctx, hipMalloc((void**)p, n ? n * sizeof(T) : 16));
+    HIP_TRY(ctx, hipMemset(*p, 0, n ? n * sizeof(T) : 16));
+    return 0;
+}
+
+}  // namespace
+
+// =======================================================================================
+// C ABI
+// =======================================================================================
+extern "C" {
+
+const char* xh_last_error(const xh_ctx* ctx) { return ctx ? ctx->err.c_str() : g_create_error.c_str(); }
+
+int xh_create(const xh_config* cfg, int device_ordinal, xh_ctx** out) {
+    if (!cfg || !out) return set_err(nullptr, XH_E_INVALID, "null argument");
+    *out = nullptr;
+    const xh_config& c = *cfg;
+    if (c.dim <= 0 || c.hidden_dim <= 0 || c.head_dim <= 0 || c.n_layers <= 0 || c.n_heads <= 0 ||
+        c.n_kv_heads <= 0 || c.vocab_size <= 0 || c.max_seq_len <= 2)
+        return set_err(nullptr, XH_E_INVALID, "bad config dims");
+    if (c.dim % 32 || c.hidden_dim % 32 || c.head_dim % 16 || (c.n_heads * c.head_dim) % 32)
+        return set_err(nullptr, XH_E_INVALID, "dims must be multiples of 32 (head_dim of 16), as the reference asserts");
+    if (c.n_heads % c.n_kv_heads) return set_err(nullptr, XH_E_INVALID, "n_heads %% n_kv_heads != 0");
+    const int qpk = c.n_heads / c.n_kv_heads;
+    if (!(qpk == 1 || qpk == 2 || qpk == 4 || qpk == 8))
+        return set_err(nullptr, XH_E_INVALID, "q heads per kv head must be 1, 2, 4 or 8 (got %d)", qpk);
+    if (!(c.head_dim == 16 || c.head_dim == 32 || c.head_dim == 64 || c.head_dim == 128 || c.head_dim == 256))
+        return set_err(nullptr, XH_E_INVALID, "head_dim must be 16..256 power of two (got %d)", c.head_dim);
+    if (c.rotary_dim > c.head_dim || c.rotary_dim < 0) return set_err(nullptr, XH_E_INVALID, "bad rotary_dim");
+    if (c.act != XH_ACT_GELU && c.act != XH_ACT_SILU) return set_err(nullptr, XH_E_INVALID, "bad act");
+
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+        return set_err(nullptr, XH_E_HIP, "no HIP device available");
+    if (device_ordinal < 0 || device_ordinal >= ndev)
+        return set_err(nullptr, XH_E_INVALID, "device %d out of range (%d devices)", device_ordinal, ndev);
+
+    xh_ctx* ctx = new xh_ctx();
+    ctx->c = c;
+    ctx->dev = device_ordinal;
+    ctx->L.resize(c.n_layers);
+    ctx->q_dim = c.n_heads * c.head_dim;
+    ctx->kv_dim = c.n_kv_heads * c.head_dim;
+    ctx->qpk = qpk;
+    ctx->nsplit = attn_nsplit(c.n_kv_heads, c.max_seq_len);
+    ctx->t_max = attn_split_len(c.max_seq_len, ctx->nsplit);
+    int rc = 0;
+#define CREATE_TRY(expr) do { rc = (expr); if (rc) { g_create_error = ctx->err; xh_destroy(ctx); return rc; } } while (0)
+    if (hipSetDevice(device_ordinal) != hipSuccess) { delete ctx; return set_err(nullptr, XH_E_HIP, "hipSetDevice failed"); }
+    if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete ctx;
+        return set_err(nullptr, XH_E_HIP, "stream create failed");
+    }
+    CREATE_TRY(dmalloc(ctx, &ctx->kv, (size_t)c.n_layers * 2 * c.max_seq_len * ctx->kv_dim));
+    CREATE_TRY(dmalloc(ctx, &ctx->x, (size_t)c.dim));
+    CREATE_TRY(dmalloc(ctx, &ctx->q, (size_t)ctx->q_dim));
+    CREATE_TRY(dmalloc(ctx, &ctx->attn_out, (size_t)ctx->q_dim));
+    CREATE_TRY(dmalloc(ctx, &ctx->hb, (size_t)c.hidden_dim));
+    CREATE_TRY(dmalloc(ctx, &ctx->logits, (size_t)c.vocab_size));
+    CREATE_TRY(dmalloc(ctx, &ctx->part_o, (size_t)ctx->nsplit * ctx->q_dim));
+    CREATE_TRY(dmalloc(ctx, &ctx->part_ml, (size_t)ctx->nsplit * c.n_heads * 2));
+    CREATE_TRY(dmalloc(ctx, &ctx->rope_freq, (size_t)c.head_dim / 2));
+    CREATE_TRY(dmalloc(ctx, &ctx->sink_cos, (size_t)c.head_dim / 2));
+    CREATE_TRY(dmalloc(ctx, &ctx->sink_sin, (size_t)c.head_dim / 2));
+    CREATE_TRY(dmalloc(ctx, &ctx->sp, 1));
+    ctx->dec_cap = 1 << 16;
+    CREATE_TRY(dmalloc(ctx, &ctx->dec_tokens, (size_t)ctx->dec_cap));
+    if (hipHostMalloc((void**)&ctx->sp_host, sizeof(StepParams), hipHostMallocDefault) != hipSuccess) {
+        g_create_error = "hipHostMalloc failed";
+        xh_destroy(ctx);
+        return XH_E_HIP;
+    }
+    memset(ctx->sp_host, 0, sizeof(StepParams));
+    ctx->sp_host->max_seq_len = c.max_seq_len;
+    // rope frequencies with the host libm, exactly the reference expression (src/infer.cpp:310-312)
+    std::vector<float> fr(c.head_dim / 2), sc(c.head_dim / 2), sn(c.head_dim / 2);
+    for (int j = 0; j < c.head_dim; j += 2) {
+        const float freq = j >= c.rotary_dim ? 0.f : 1.0f / powf(c.rope_theta, (float)j / (float)c.rotary_dim);
+        fr[j / 2] = freq;
+        const float val = 1 * freq;  // sink re-rotation: rope at pos = 1 (src/infer.cpp:426)
+        sc[j / 2] = cosf(val);
+        sn[j / 2] = sinf(val);
+    }
+    if (hipMemcpy(ctx->rope_freq, fr.data(), fr.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(ctx->sink_cos, sc.data(), sc.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(ctx->sink_sin, sn.data(), sn.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(ctx->sp, ctx->sp_host, sizeof(StepParams), hipMemcpyHostToDevice) != hipSuccess) {
+        g_create_error = "initial copies failed";
+        xh_destroy(ctx);
+        return XH_E_HIP;
+    }
+#undef CREATE_TRY
+    *out = ctx;
+    return 0;
+}
+
+void xh_destroy(xh_ctx* ctx) {
+    if (!ctx) return;
+    hipSetDevice(ctx->dev);
+    if (ctx->stream) hipStreamSynchronize(ctx->stream);
+    drop_graphs(ctx);
+    for (auto& w : ctx->L) {
+        hipFree(w.wqkv); hipFree(w.w13); hipFree(w.wo); hipFree(w.w2); hipFree(w.attn_norm); hipFree(w.ffn_norm);
+    }
+    if (ctx->wcls && ctx->wcls != ctx->embed) hipFree(ctx->wcls);
+    hipFree(ctx->embed); hipFree(ctx->final_norm);
+    hipFree(ctx->kv); hipFree(ctx->x); hipFree(ctx->q); hipFree(ctx->attn_out); hipFree(ctx->hb);
+    hipFree(ctx->logits); hipFree(ctx->part_o); hipFree(ctx->part_ml); hipFree(ctx->rope_freq);
+    hipFree(ctx->sink_cos); hipFree(ctx->sink_sin); hipFree(ctx->sp); hipFree(ctx->dec_tokens);
+    if (ctx->sp_host) hipHostFree(ctx->sp_host);
+    if (ctx->stream) hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+}  // extern "C"
+
+namespace {
+
+// Destination of one logical tensor [rows][cols] inside the device layout: the buffer
+// (allocated on first use), the byte offset of row 0 and the byte pitch between rows.
+struct Slot {
+    char* base = nullptr;
+    size_t pitch = 0;
+    size_t rows = 0, cols = 0;
+};
+
+int tensor_slot(xh_ctx* ctx, int kind, int layer, int dtype, Slot* out) {
+    const xh_config& c = ctx->c;
+    const bool per_layer = !(kind == XH_EMBED || kind == XH_FINAL_NORM || kind == XH_WCLS);
+    if (per_layer && (layer < 0 || layer >= c.n_layers))
+        return set_err(ctx, XH_E_INVALID, "layer %d out of range", layer);
+    size_t rows = 0, cols = 0;
+    bool is_norm = false;
+    switch (kind) {
+        case XH_EMBED: case XH_WCLS: rows = c.vocab_size; cols = c.dim; break;
+        case XH_ATTN_NORM: case XH_FFN_NORM: case XH_FINAL_NORM: rows = 1; cols = c.dim; is_norm = true; break;
+        case XH_WQ: rows = ctx->q_dim; cols = c.dim; break;
+        case XH_WK: case XH_WV: rows = ctx->kv_dim; cols = c.dim; break;
+        case XH_WO: rows = c.dim; cols = ctx->q_dim; break;
+        case XH_W1: case XH_W3: rows = c.hidden_dim; cols = c.dim; break;
+        case XH_W2: rows = c.dim; cols = c.hidden_dim; break;
+        default: return set_err(ctx, XH_E_INVALID, "unknown tensor kind %d", kind);
+    }
+    if (is_norm ? !(dtype == XH_F32 || dtype == XH_BF16) : !matrix_dtype_ok(dtype))
+        return set_err(ctx, XH_E_INVALID, "tensor kind %d: unsupported dtype %d", kind, dtype);
+    const size_t rb = cols * dtype_size(dtype);
+    out->rows = rows;
+    out->cols = cols;
+    out->pitch = rb;
+    drop_graphs(ctx);
+    auto plain = [&](void** dst, int* dst_dt) -> int {
+        if (*dst && *dst_dt != dtype) {
+            if (*dst == ctx->wcls && *dst != ctx->embed) ctx->wcls = nullptr;
+            hipFree(*dst);
+            *dst = nullptr;
+        }
+        if (!*dst) HIP_TRY(ctx, hipMalloc(dst, rows * rb));
+        *dst_dt = dtype;
+        out->base = (char*)*dst;
+        return 0;
+    };
+    if (kind == XH_EMBED) {
+        const bool alias = ctx->wcls != nullptr && ctx->wcls == ctx->embed;
+        if (alias) ctx->wcls = nullptr;
+        int rc = plain(&ctx->embed, &ctx->embed_dt);
+        if (alias) { ctx->wcls = ctx->embed; ctx->wcls_dt = ctx->embed_dt; }
+        return rc;
+    }
+    if (kind == XH_FINAL_NORM) return plain(&ctx->final_norm, &ctx->final_norm_dt);
+    if (kind == XH_WCLS) {
+        if (ctx->wcls == ctx->embed) ctx->wcls = nullptr;
+        return plain(&ctx->wcls, &ctx->wcls_dt);
+    }
+    LayerW& w = ctx->L[layer];
+    switch (kind) {
+        case XH_ATTN_NORM: return plain(&w.attn_norm, &w.an_dt);
+        case XH_FFN_NORM: return plain(&w.ffn_norm, &w.fn_dt);
+        case XH_WO: return plain(&w.wo, &w.wo_dt);
+        case XH_W2: return plain(&w.w2, &w.w2_dt);
+        case XH_WQ: case XH_WK: case XH_WV: {
+            // fused [Wq; Wk; Wv] rows, one dtype
+            if (w.wqkv && w.qkv_dt != dtype) {
+                if (w.qkv_have & ~(1u << (kind - XH_WQ)))
+                    return set_err(ctx, XH_E_INVALID, "layer %d: q/k/v must share one dtype", layer);
+                hipFree(w.wqkv); w.wqkv = nullptr; w.qkv_have = 0;
+            }
+            if (!w.wqkv) HIP_TRY(ctx, hipMalloc(&w.wqkv, (size_t)(ctx->q_dim + 2 * ctx->kv_dim) * rb));
+            w.qkv_dt = dtype;
+            const size_t row0 = kind == XH_WQ ? 0 : kind == XH_WK ? ctx->q_dim : ctx->q_dim + ctx->kv_dim;
+            out->base = (char*)w.wqkv + row0 * rb;
+            w.qkv_have |= 1u << (kind - XH_WQ);
+            return 0;
+        }
+        case XH_W1: case XH_W3: {
+            // fused gate/up, rows interleaved: row 2i = W1[i], row 2i+1 = W3[i]
+            const unsigned bit = kind == XH_W1 ? 1u : 2u;
+            if (w.w13 && w.w13_dt != dtype) {
+                if (w.w13_have & ~bit) return set_err(ctx, XH_E_INVALID, "layer %d: w1/w3 must share one dtype", layer);
+                hipFree(w.w13); w.w13 = nullptr; w.w13_have = 0;
+            }
+            if (!w.w13) HIP_TRY(ctx, hipMalloc(&w.w13, (size_t)2 * c.hidden_dim * rb));
+            w.w13_dt = dtype;
+            out->base = (char*)w.w13 + (kind == XH_W3 ? rb : 0);
+            out->pitch = 2 * rb;
+            w.w13_have |= bit;
+            return 0;
+        }
+    }
+    return set_err(ctx, XH_E_INVALID, "unhandled kind");
+}
+
+__global__ void synth_fill_kernel(char* base, size_t pitch, size_t rows, size_t cols, int dtype, uint64_t seed,
+                                  float mean, float std) {
+    const size_t n = rows * cols;
+    const size_t esz = dtype == XH_F32 ? 4 : (dtype == XH_F16 || dtype == XH_BF16) ? 2 : 1;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        const size_t r = i / cols, cidx = i - r * cols;
+        xs_store(base + r * pitch, cidx, dtype, xs_value(seed, i, mean, std));
+        (void)esz;
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+int xh_upload(xh_ctx* ctx, int kind, int layer, int dtype, const void* host, size_t bytes) {
+    if (!ctx || !host) return set_err(ctx, XH_E_INVALID, "null argument");
+    HIP_TRY(ctx, hipSetDevice(ctx->dev));
+    Slot s;
+    // validate the byte count before touching the device layout
+    {
+        const xh_config& c = ctx->c;
+        size_t rows = 0, cols = 0;
+        switch (kind) {
+            case XH_EMBED: case XH_WCLS: rows = c.vocab_size; cols = c.dim; break;
+            case XH_ATTN_NORM: case XH_FFN_NORM: case XH_FINAL_NORM: rows = 1; cols = c.dim; break;
+            case XH_WQ: rows = ctx->q_dim; cols = c.dim; break;
+            case XH_WK: case XH_WV: rows = ctx->kv_dim; cols = c.dim; break;
+            case XH_WO: rows = c.dim; cols = ctx->q_dim; break;
+            case XH_W1: case XH_W3: rows = c.hidden_dim; cols = c.dim; break;
+            case XH_W2: rows = c.dim; cols = c.hidden_dim; break;
+            default: return set_err(ctx, XH_E_INVALID, "unknown tensor kind %d", kind);
+        }
+        const size_t esz = dtype_size(dtype);
+        if (esz == 0 || bytes != rows * cols * esz)
+            return set_err(ctx, XH_E_INVALID, "tensor kind %d: %zu bytes, expected %zu ([%zu,%zu] of dtype %d)", kind,
+                           bytes, rows * cols * esz, rows, cols, dtype);
+    }
+    int rc = tensor_slot(ctx, kind, layer, dtype, &s);
+    if (rc) return rc;
+    HIP_TRY(ctx, hipMemcpy2D(s.base, s.pitch, host, s.cols * dtype_size(dtype), s.cols * dtype_size(dtype), s.rows,
+                             hipMemcpyHostToDevice));
+    return 0;
+}
+
+int xh_upload_synthetic(xh_ctx* ctx, int kind, int layer, int dtype, uint64_t seed, float mean, float std) {
+    if (!ctx) return XH_E_INVALID;
+    if (dtype == XH_Q8) return set_err(ctx, XH_E_INVALID, "no synthetic Q8");
+    HIP_TRY(ctx, hipSetDevice(ctx->dev));
+    Slot s;
+    int rc = tensor_slot(ctx, kind, layer, dtype, &s);
+    if (rc) return rc;
+    hipLaunchKernelGGL(synth_fill_kernel, dim3(4096), dim3(256), 0, ctx->stream, s.base, s.pitch, s.rows, s.cols, dtype,
+                       seed, mean, std);
+    HIP_TRY(ctx, hipGetLastError());
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    return 0;
+}
+
+int xh_kv_fill_synthetic(xh_ctx* ctx, int layer, int which, int slot0, int n_slots, uint64_t seed, float std) {
+    if (!ctx || layer < 0 || layer >= ctx->c.n_layers || (which != 0 && which != 1) || slot0 < 0 || n_slots < 0 ||
+        slot0 + n_slots > ctx->c.max_seq_len)
+        return set_err(ctx, XH_E_INVALID, "bad kv_fill_synthetic arguments");
+    HIP_TRY(ctx, hipSetDevice(ctx->dev));
+    char* base = (char*)((which ? ctx->vcache(layer) : ctx->kcache(layer)) + (size_t)slot0 * ctx->kv_dim);
+    hipLaunchKernelGGL(synth_fill_kernel, dim3(2048), dim3(256), 0, ctx->stream, base, (size_t)ctx->kv_dim * 2,
+                       (size_t)n_slots, (size_t)ctx->kv_dim, (int)XH_F16, seed, 0.0f, std);
+    HIP_TRY(ctx, hipGetLastError());
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    return 0;
+}
+
+int xh_forward(xh_ctx* ctx, int token, int pos, int mode, float* logits_out) {
+    if (!ctx) return XH_E_INVALID;
+    if (token < 0 || token >= ctx->c.vocab_size) return set_err(ctx, XH_E_INVALID, "token %d out of range", token);
+    if (pos < 0) return set_err(ctx, XH_E_INVALID, "negative pos");
+    if (mode != XH_HYDRATE_KV_CACHE && mode != XH_OUTPUT_LOGITS) return set_err(ctx, XH_E_INVALID, "bad mode");
+    HIP_TRY(ctx, hipSetDevice(ctx->dev));
+    int rc = check_ready(ctx);
+    if (rc) return rc;
+    rc = host_step_params(ctx, token, pos);
+    if (rc) return rc;
+    rc = run_step(ctx, mode == XH_OUTPUT_LOGITS);
+    if (rc) return rc;
+    if (logits_out && mode == XH_OUTPUT_LOGITS)
+        HIP_TRY(ctx, hipMemcpyAsync(logits_out, ctx->logits, (size_t)ctx->c.vocab_size * 4, hipMemcpyDeviceToHost,
+                                    ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    return 0;
+}
+
+int xh_decode_greedy(xh_ctx* ctx, int pos, int n_steps, int stop_a, int stop_b, int* tokens_out, int* n_done) {
+    if (!ctx || n_steps < 0) return XH_E_INVALID;
+    if (n_done) *n_done = 0;
+    if (n_steps > ctx->dec_cap) return set_err(ctx, XH_E_INVALID, "n_steps > %d", ctx->dec_cap);
+    HIP_TRY(ctx, hipSetDevice(ctx->dev));
+    int rc = check_ready(ctx);
+    if (rc) return rc;
+    // step counter 0, next position `pos`; token/pos fields are set by argmax_advance_kernel
+    StepParams* h = ctx->sp_host;
+    h->step = 0;
+    h->pos_next = pos;
+    h->max_seq_len = ctx->c.max_seq_len;
+    HIP_TRY(ctx, hipMemcpyAsync(&ctx->sp->step, &h->step, 3 * sizeof(int), hipMemcpyHostToDevice, ctx->stream));
+    if (ctx->use_graphs && !ctx->g_decode) {
+        rc = capture(ctx, 2, &ctx->g_decode);
+        if (rc) return rc;
+    }
+    const bool stops = stop_a >= 0 || stop_b >= 0;
+    int done = 0;
+    for (int i = 0; i < n_steps; i++) {
+        if (ctx->use_graphs) {
+            HIP_TRY(ctx, hipGraphLaunch(ctx->g_decode, ctx->stream));
+        } else {
+            hipLaunchKernelGGL(argmax_advance_kernel, dim3(1), dim3(1024), 0, ctx->stream, (const float*)ctx->logits,
+                               ctx->c.vocab_size, ctx->sp, ctx->dec_tokens, ctx->dec_cap);
+            rc = enqueue_step(ctx, ctx->stream, true);
+            if (rc) return rc;
+        }
+        done = i + 1;
+        if (stops) {
+            int tok = -1;
+            HIP_TRY(ctx, hipMemcpyAsync(&tok, ctx->dec_tokens + i, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+            HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+            if (tok == stop_a || tok == stop_b) break;
+        }
+    }
+    if (tokens_out && done)
+        HIP_TRY(ctx, hipMemcpyAsync(tokens_out, ctx->dec_tokens, (size_t)done * sizeof(int), hipMemcpyDeviceToHost,
+                                    ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    if (n_done) *n_done = done;
+    return 0;
+}
+
+int xh_get_logits(xh_ctx* ctx, float* logits_out) {
+    if (!ctx || !logits_out) return XH_E_INVALID;
+    HIP_TRY(ctx, hipSetDevice(ctx->dev));
+    HIP_TRY(ctx, hipMemcpyAsync(logits_out, ctx->logits, (size_t)ctx->c.vocab_size * 4, hipMemcpyDeviceToHost,
+                                ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    return 0;
+}
+
+int xh_reset(xh_ctx* ctx) {
+    if (!ctx) return XH_E_INVALID;
+    HIP_TRY(ctx, hipSetDevice(ctx->dev));
+    const xh_config& c = ctx->c;
+    HIP_TRY(ctx, hipMemsetAsync(ctx->kv, 0, (size_t)c.n_layers * 2 * c.max_seq_len * ctx->kv_dim * 2, ctx->stream));
+    HIP_TRY(ctx, hipMemsetAsync(ctx->x, 0, (size_t)c.dim * 4, ctx->stream));
+    HIP_TRY(ctx, hipMemsetAsync(ctx->logits, 0, (size_t)c.vocab_size * 4, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    return 0;
+}
+
+int xh_kv_write(xh_ctx* ctx, int layer, int which, int slot0, int n_slots, const uint16_t* host) {
+    if (!ctx || !host || layer < 0 || layer >= ctx->c.n_layers || (which != 0 && which != 1) || slot0 < 0 ||
+        n_slots < 0 || slot0 + n_slots > ctx->c.max_seq_len)
+        return set_err(ctx, XH_E_INVALID, "bad kv_write arguments");
+    HIP_TRY(ctx, hipSetDevice(ctx->dev));
+    uint16_t* base = (which ? ctx->vcache(layer) : ctx->kcache(layer)) + (size_t)slot0 * ctx->kv_dim;
+    HIP_TRY(ctx, hipMemcpy(base, host, (size_t)n_slots * ctx->kv_dim * 2, hipMemcpyHostToDevice));
+    return 0;
+}
+
+int xh_kv_read(xh_ctx* ctx, int layer, int which, int slot0, int n_slots, uint16_t* host) {
+    if (!ctx || !host || layer < 0 || layer >= ctx->c.n_layers || (which != 0 && which != 1) || slot0 < 0 ||
+        n_slots < 0 || slot0 + n_slots > ctx->c.max_seq_len)
+        return set_err(ctx, XH_E_INVALID, "bad kv_read arguments");
+    HIP_TRY(ctx, hipSetDevice(ctx->dev));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    const uint16_t* base = (which ? ctx->vcache(layer) : ctx->kcache(layer)) + (size_t)slot0 * ctx->kv_dim;
+    HIP_TRY(ctx, hipMemcpy(host, base, (size_t)n_slots * ctx->kv_dim * 2, hipMemcpyDeviceToHost));
+    return 0;
+}
+
+size_t xh_active_bytes(const xh_ctx* ctx, size_t pos) {
+    // Model::active_bytes, src/model.cpp:12-35
+    if (!ctx) return 0;
+    const xh_config& c = ctx->c;
+    size_t bytes = (size_t)c.dim * dtype_size(ctx->embed_dt);
+    bytes += (size_t)c.dim * dtype_size(ctx->final_norm_dt);
+    const int wdt = ctx->wcls ? ctx->wcls_dt : ctx->embed_dt;
+    bytes += (size_t)c.vocab_size * c.dim * dtype_size(wdt);
+    const size_t kv_len = (size_t)c.max_seq_len < pos + 1 ? (size_t)c.max_seq_len : pos + 1;
+    for (int l = 0; l < c.n_layers; ++l) {
+        const LayerW& w = ctx->L[l];
+        bytes += (size_t)c.dim * dtype_size(w.an_dt) + (size_t)c.dim * dtype_size(w.fn_dt);
+        bytes += (size_t)(ctx->q_dim + 2 * ctx->kv_dim) * c.dim * dtype_size(w.qkv_dt);
+        bytes += (size_t)ctx->q_dim * c.dim * dtype_size(w.wo_dt);
+        bytes += (size_t)2 * c.hidden_dim * c.dim * dtype_size(w.w13_dt);
+        bytes += (size_t)c.hidden_dim * c.dim * dtype_size(w.w2_dt);
+        bytes += 2 * kv_len * ctx->kv_dim * 2;
+    }
+    return bytes;
+}
+
+int xh_set_graphs(xh_ctx* ctx, int enable) {
+    if (!ctx) return XH_E_INVALID;
+    ctx->use_graphs = enable != 0;
+    if (!ctx->use_graphs) drop_graphs(ctx);
+    return 0;
+}
+
+// ---------------------------------------------------------------------------------------
+// exposed-for-tests ops (host pointers).  They run the same kernels as the forward pass.
+// ---------------------------------------------------------------------------------------
+namespace {
+struct DevBuf {
+    void* p = nullptr;
+    ~DevBuf() { if (p) hipFree(p); }
+};
+int op_alloc(DevBuf& b, size_t bytes, const void* src) {
+    if (hipMalloc(&b.p, bytes ? bytes : 16) != hipSuccess) return set_err(nullptr, XH_E_HIP, "hipMalloc failed");
+    if (src && hipMemcpy(b.p, src, bytes, hipMemcpyHostToDevice) != hipSuccess)
+        return set_err(nullptr, XH_E_HIP, "hipMemcpy failed");
+    return 0;
+}
+int op_finish(void* dst, const DevBuf& b, size_t bytes) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return set_err(nullptr, XH_E_HIP, "kernel launch failed: %s", hipGetErrorString(e));
+    if (hipDeviceSynchronize() != hipSuccess) return set_err(nullptr, XH_E_HIP, "kernel failed");
+    if (hipMemcpy(dst, b.p, bytes, hipMemcpyDeviceToHost) != hipSuccess)
+        return set_err(nullptr, XH_E_HIP, "hipMemcpy D2H failed");
+    return 0;
+}
+}  // namespace
+
+int xh_op_matmul(float* xout, const float* x, const void* w, int dtype, int n, int d) {
+    if (!xout || !x || !w || n <= 0 || d <= 0 || n % 16) return set_err(nullptr, XH_E_INVALID, "bad matmul args");
+    if (!matrix_dtype_ok(dtype)) return set_err(nullptr, XH_E_INVALID, "unsupported dtype %d", dtype);
+    DevBuf bw, bx, bo;
+    int rc;
+    const size_t wbytes = (size_t)n * d * dtype_size(dtype);
+    if ((rc = op_alloc(bw, wbytes, w)) || (rc = op_alloc(bx, (size_t)n * 4, x)) || (rc = op_alloc(bo, (size_t)d * 4, nullptr)))
+        return rc;
+    GemvArgs a{};
+    a.w = bw.p; a.row_bytes = (size_t)n * dtype_size(dtype); a.n = n; a.rows = d;
+    a.x = (const float*)bx.p; a.out = (float*)bo.p;
+    launch_gemv<PRO_PLAIN, EPI_STORE>(dtype, a, nullptr, 1024);
+    return op_finish(xout, bo, (size_t)d * 4);
+}
+
+int xh_op_rmsnorm(float* o, const float* x, const void* weight, int dtype, int size, float eps) {
+    if (!o || !x || !weight || size <= 0 || size % 4 || !(dtype == XH_F32 || dtype == XH_BF16))
+        return set_err(nullptr, XH_E_INVALID, "bad rmsnorm args");
+    DevBuf bw, bx, bo;
+    int rc;
+    if ((rc = op_alloc(bw, (size_t)size * dtype_size(dtype), weight)) || (rc = op_alloc(bx, (size_t)size * 4, x)) ||
+        (rc = op_alloc(bo, (size_t)size * 4, nullptr)))
+        return rc;
+    hipLaunchKernelGGL(rmsnorm_kernel, dim3(1), dim3(GEMV_THREADS), 0, nullptr, (float*)bo.p, (const float*)bx.p,
+                       (const void*)bw.p, dtype, size, eps);
+    return op_finish(o, bo, (size_t)size * 4);
+}
+
+int xh_op_rope(float* vec, int d, int head_dim, int pos, float theta, int rotary_dim) {
+    if (!vec || d <= 0 || d % 2 || head_dim <= 0 || head_dim % 2) return set_err(nullptr, XH_E_INVALID, "bad rope args");
+    std::vector<float> fr(head_dim / 2);
+    for (int j = 0; j < head_dim; j += 2)
+        fr[j / 2] = j >= rotary_dim ? 0.f : 1.0f / powf(theta, (float)j / (float)rotary_dim);
+    DevBuf bv, bf;
+    int rc;
+    if ((rc = op_alloc(bv, (size_t)d * 4, vec)) || (rc = op_alloc(bf, fr.size() * 4, fr.data()))) return rc;
+    hipLaunchKernelGGL(rope_kernel, dim3((d / 2 + 255) / 256), dim3(256), 0, nullptr, (float*)bv.p, d, head_dim, pos,
+                       (const float*)bf.p);
+    return op_finish(vec, bv, (size_t)d * 4);
+}
+
+int xh_op_mha(float* xout, const uint16_t* kb, const uint16_t* vb, const float* q, int head_dim, int kv_len,
+              int max_seq_len, int n_heads, int n_kv_heads) {
+    if (!xout || !kb || !vb || !q || kv_len <= 0 || kv_len > max_seq_len || n_kv_heads <= 0 || n_heads % n_kv_heads)
+        return set_err(nullptr, XH_E_INVALID, "bad mha args");
+    const int qpk = n_heads / n_kv_heads, kv_dim = n_kv_heads * head_dim;
+    const int nsplit = attn_nsplit(n_kv_heads, max_seq_len);
+    const int t_max = attn_split_len(max_seq_len, nsplit);
+    DevBuf bk, bv, bq, bo, bpo, bpm, bsp;
+    StepParams sp{};
+    sp.kv_len = kv_len;
+    sp.max_seq_len = max_seq_len;
+    int rc;
+    const size_t kvb = (size_t)max_seq_len * kv_dim * 2;
+    if ((rc = op_alloc(bk, kvb, kb)) || (rc = op_alloc(bv, kvb, vb)) || (rc = op_alloc(bq, (size_t)n_heads * head_dim * 4, q)) ||
+        (rc = op_alloc(bo, (size_t)n_heads * head_dim * 4, nullptr)) ||
+        (rc = op_alloc(bpo, (size_t)nsplit * n_heads * head_dim * 4, nullptr)) ||
+        (rc = op_alloc(bpm, (size_t)nsplit * n_heads * 2 * 4, nullptr)) || (rc = op_alloc(bsp, sizeof sp, &sp)))
+        return rc;
+    AttnArgs a{};
+    a.q = (const float*)bq.p; a.kc = (const uint16_t*)bk.p; a.vc = (const uint16_t*)bv.p; a.kv_dim = kv_dim;
+    a.n_heads = n_heads; a.nsplit = nsplit; a.out = (float*)bo.p; a.part_o = (float*)bpo.p;
+    a.part_ml = (float*)bpm.p; a.sp = (const StepParams*)bsp.p;
+    if (!launch_attn(a, head_dim, qpk, n_kv_heads, t_max, nullptr))
+        return set_err(nullptr, XH_E_INVALID, "unsupported head_dim %d / qpk %d", head_dim, qpk);
+    return op_finish(xout, bo, (size_t)n_heads * head_dim * 4);
+}
+
+// ---------------------------------------------------------------------------------------
+// timing hooks for bench.py
+// ---------------------------------------------------------------------------------------
+int xh_time_kernel(xh_ctx* ctx, int which, int iters, float* avg_us) {
+    if (!ctx || !avg_us || iters <= 0 || which < 0 || which > 5) return XH_E_INVALID;
+    HIP_TRY(ctx, hipSetDevice(ctx->dev));
+    int rc = check_ready(ctx);
+    if (rc) return rc;
+    const int mb = ctx->max_gemv_blocks;
+    auto launch = [&]() -> bool {
+        switch (which) {
+            case 0: return launch_gemv<PRO_RMSNORM, EPI_GLU>(ctx->L[0].w13_dt, w13_args(ctx, 0), ctx->stream, mb);
+            case 1: return launch_gemv<PRO_RMSNORM, EPI_QKV>(ctx->L[0].qkv_dt, qkv_args(ctx, 0), ctx->stream, mb);
+            case 2: return launch_gemv<PRO_PLAIN, EPI_RESID>(ctx->L[0].wo_dt, wo_args(ctx, 0), ctx->stream, mb);
+            case 3: return launch_gemv<PRO_PLAIN, EPI_RESID>(ctx->L[0].w2_dt, w2_args(ctx, 0), ctx->stream, mb);
+            case 4: return launch_gemv<PRO_RMSNORM, EPI_STORE>(ctx->wcls_dt, cls_args(ctx), ctx->stream, mb);
+            default:
+                return launch_attn(attn_args(ctx, 0), ctx->c.head_dim, ctx->qpk, ctx->c.n_kv_heads, ctx->t_max,
+                                   ctx->stream);
+        }
+    };
+    hipEvent_t e0, e1;
+    HIP_TRY(ctx, hipEventCreate(&e0));
+    HIP_TRY(ctx, hipEventCreate(&e1));
+    for (int i = 0; i < 3; i++) launch();
+    HIP_TRY(ctx, hipEventRecord(e0, ctx->stream));
+    for (int i = 0; i < iters; i++) launch();
+    HIP_TRY(ctx, hipEventRecord(e1, ctx->stream));
+    HIP_TRY(ctx, hipEventSynchronize(e1));
+    float ms = 0.f;
+    HIP_TRY(ctx, hipEventElapsedTime(&ms, e0, e1));
+    hipEventDestroy(e0);
+    hipEventDestroy(e1);
+    HIP_TRY(ctx, hipGetLastError());
+    *avg_us = ms * 1000.f / (float)iters;
+    return 0;
+}
+
+size_t xh_kernel_bytes(const xh_ctx* ctx, int which, int kv_len) {
+    if (!ctx) return 0;
+    const xh_config& c = ctx->c;
+    const LayerW& w = ctx->L[0];
+    const size_t vec = 4;
+    switch (which) {
+        case 0: return (size_t)2 * c.hidden_dim * c.dim * dtype_size(w.w13_dt) + c.dim * (vec + dtype_size(w.fn_dt)) +
+                       (size_t)c.hidden_dim * vec;
+        case 1: return (size_t)(ctx->q_dim + 2 * ctx->kv_dim) * c.dim * dtype_size(w.qkv_dt) +
+                       c.dim * (vec + dtype_size(w.an_dt)) + (size_t)ctx->q_dim * vec + 2 * ctx->kv_dim * 2;
+        case 2: return (size_t)ctx->q_dim * c.dim * dtype_size(w.wo_dt) + ctx->q_dim * vec + 2 * c.dim * vec;
+        case 3: return (size_t)c.hidden_dim * c.dim * dtype_size(w.w2_dt) + c.hidden_dim * vec + 2 * c.dim * vec;
+        case 4: return (size_t)c.vocab_size * c.dim * dtype_size(ctx->wcls ? ctx->wcls_dt : ctx->embed_dt) +
+                       c.dim * (vec + dtype_size(ctx->final_norm_dt)) + (size_t)c.vocab_size * vec;
+        default: return (size_t)2 * kv_len * ctx->kv_dim * 2 + 2 * (size_t)ctx->q_dim * vec;
+    }
+}
+
+}  // extern "C"
