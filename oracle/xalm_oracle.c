@@ -132,7 +132,9 @@ static size_t dtype_bits(int dtype) {
  * implementation-defined; here 8-wide FMA lanes for f16). */
 void xo_matmul(float* xout, const float* x, const void* w, const int dtype, const int n, const int d) {
     int i;
-    if (dtype == XH_F16) {
+    static int scalar_order = -1; /* XO_MATMUL_SCALAR=1: sequential in-row order (sensitivity checks) */
+    if (scalar_order < 0) scalar_order = getenv("XO_MATMUL_SCALAR") && atoi(getenv("XO_MATMUL_SCALAR"));
+    if (dtype == XH_F16 && !scalar_order) {
         const uint16_t* W = (const uint16_t*)w;
 #pragma omp parallel for schedule(static)
         for (i = 0; i < d; i++) {
@@ -173,6 +175,7 @@ void xo_matmul(float* xout, const float* x, const void* w, const int dtype, cons
 #define DEC_F32(v) (v)
     switch (dtype) {
         case XH_F32: XO_MATMUL_LOOP(float, DEC_F32); break;
+        case XH_F16: XO_MATMUL_LOOP(uint16_t, xo_f16_to_f32); break;
         case XH_BF16: XO_MATMUL_LOOP(uint16_t, bf16_to_f32); break;
         case XH_F8_E4M3: XO_MATMUL_LOOP(uint8_t, f8e4m3_to_f32); break;
         case XH_F8_E5M2: XO_MATMUL_LOOP(uint8_t, f8e5m2_to_f32); break;

@@ -20,7 +20,7 @@ STEPS=${STEPS:-smoke tests bench prof}
 for s in $STEPS; do
     case $s in
         smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
-        tests) run pytest_gpu 900 python -m pytest tests -m gpu -q -p pytest_timeout --timeout 300 -rf ;;
+        tests) run pytest_gpu 900 python -m pytest tests -m gpu -q --timeout 300 -rf ;;
         bench) run bench 600 python bench.py ;;
         bench_f8) run bench_f8 600 python bench.py --workload mistral-7b-f8 ;;
         bench_32k) run bench_32k 600 python bench.py --workload mistral-7b-f16-32k --steps 64 ;;

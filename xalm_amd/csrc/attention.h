@@ -7,8 +7,12 @@
 //   o_h = sum_t p_t V[t, g],   g = h / (n_heads / n_kv_heads)
 // One workgroup serves one KV head and a contiguous slot range, so each K/V row is read from
 // HBM once for all q heads of its group (the CPU re-reads it per q head).  The slot range
-// length T is chosen on device from kv_len so the grid shape never changes (graph replay).
-// With more than one active split, partial (o, m, l) are merged by attn_combine_kernel.
+// length T is chosen on device from kv_len, so the grid never changes (graph replay).
+// K and V rows of the first PREF passes are requested together at kernel start: for contexts
+// up to 64 * nsplit slots the whole kernel is one HBM round trip.
+// With more than one active split, every block stores its partial (o, m, l); the last block
+// of each KV head to arrive (agent-scope release -> ticket -> acquire, cdna_hip_programming.md
+// §6 Guideline 16 / "In-launch split-K reduction") merges them: no second launch.
 #pragma once
 
 #include <float.h>
@@ -18,6 +22,8 @@
 namespace xalm {
 
 constexpr int ATTN_THREADS = 256;
+constexpr int ATTN_PREF = 4;     // K/V passes held in registers per round
+constexpr int ATTN_MIN_T = 64;   // minimum slots per split
 
 struct AttnArgs {
     const float* q;          // [n_heads * HD], roped
@@ -29,14 +35,15 @@ struct AttnArgs {
     float* out;              // [n_heads * HD]
     float* part_o;           // [nsplit][n_heads][HD]
     float* part_ml;          // [nsplit][n_heads][2]
+    int* counters;           // [n_kv_heads], zero between launches
     const StepParams* sp;
 };
 
-// slots per split for this step: >= 16, multiple of 16, nsplit * T >= kv_len
+// slots per split for this step: >= ATTN_MIN_T, multiple of 16, nsplit * T >= kv_len
 __device__ __host__ __forceinline__ int attn_split_len(const int kv_len, const int nsplit) {
     int t = (kv_len + nsplit - 1) / nsplit;
     t = (t + 15) & ~15;
-    return t < 16 ? 16 : t;
+    return t < ATTN_MIN_T ? ATTN_MIN_T : t;
 }
 
 template <int HD, int QPK>
@@ -45,8 +52,9 @@ __global__ __launch_bounds__(ATTN_THREADS) void attn_split_kernel(const AttnArgs
     constexpr int RPP = ATTN_THREADS / LPR;   // rows per pass
     extern __shared__ __attribute__((aligned(16))) char smem[];
     float* red = (float*)smem;                               // [4][QPK][HD]
-    float* ml = red + 4 * QPK * HD;                          // [QPK][2]
-    float* sc = ml + ((2 * QPK + 3) & ~3);                   // [QPK][T]
+    float* ml = red + 4 * QPK * HD;                          // [QPK][2] (+ flag)
+    float* sc = ml + ((2 * QPK + 4) & ~3);                   // [QPK][T]
+    int* flag = (int*)(ml + 2 * QPK);
 
     const int kv_len = a.sp->kv_len;
     const int T = attn_split_len(kv_len, a.nsplit);
@@ -58,7 +66,18 @@ __global__ __launch_bounds__(ATTN_THREADS) void attn_split_kernel(const AttnArgs
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int sub = tid % LPR, rr = tid / LPR;
     const float scale = 1.0f / sqrtf((float)HD);  // src/infer.cpp:338
+    const size_t col = (size_t)g * HD + sub * 8;
 
+    // ---- first round of K and V rows, requested before anything else ----
+    u32x4 kr[ATTN_PREF], vr[ATTN_PREF];
+#pragma unroll
+    for (int p = 0; p < ATTN_PREF; p++) {
+        const int t = t0 + rr + p * RPP;
+        if (t < t1) {
+            kr[p] = *(const u32x4*)(a.kc + (size_t)t * a.kv_dim + col);
+            vr[p] = *(const u32x4*)(a.vc + (size_t)t * a.kv_dim + col);
+        }
+    }
     float qv[QPK][8];
 #pragma unroll
     for (int h = 0; h < QPK; h++) {
@@ -67,11 +86,9 @@ __global__ __launch_bounds__(ATTN_THREADS) void attn_split_kernel(const AttnArgs
         qv[h][0] = q0.x; qv[h][1] = q0.y; qv[h][2] = q0.z; qv[h][3] = q0.w;
         qv[h][4] = q1.x; qv[h][5] = q1.y; qv[h][6] = q1.z; qv[h][7] = q1.w;
     }
-    const size_t col = (size_t)g * HD + sub * 8;
 
     // ---- scores ----
-    for (int t = t0 + rr; t < t1; t += RPP) {
-        const u32x4 kw = *(const u32x4*)(a.kc + (size_t)t * a.kv_dim + col);
+    auto score_row = [&](const u32x4 kw, const int t) {
         float kf[8];
         WDec<XH_F16>::dec(kw, kf);
 #pragma unroll
@@ -82,6 +99,24 @@ __global__ __launch_bounds__(ATTN_THREADS) void attn_split_kernel(const AttnArgs
 #pragma unroll
             for (int o = LPR / 2; o > 0; o >>= 1) p += __shfl_xor(p, o, 64);
             if (sub == 0) sc[h * T + (t - t0)] = p * scale;
+        }
+    };
+#pragma unroll
+    for (int p = 0; p < ATTN_PREF; p++) {
+        const int t = t0 + rr + p * RPP;
+        if (t < t1) score_row(kr[p], t);
+    }
+    for (int base = t0 + ATTN_PREF * RPP; base < t1; base += ATTN_PREF * RPP) {
+        u32x4 kk[ATTN_PREF];
+#pragma unroll
+        for (int p = 0; p < ATTN_PREF; p++) {
+            const int t = base + rr + p * RPP;
+            if (t < t1) kk[p] = *(const u32x4*)(a.kc + (size_t)t * a.kv_dim + col);
+        }
+#pragma unroll
+        for (int p = 0; p < ATTN_PREF; p++) {
+            const int t = base + rr + p * RPP;
+            if (t < t1) score_row(kk[p], t);
         }
     }
     __syncthreads();
@@ -109,8 +144,7 @@ __global__ __launch_bounds__(ATTN_THREADS) void attn_split_kernel(const AttnArgs
     for (int h = 0; h < QPK; h++)
 #pragma unroll
         for (int i = 0; i < 8; i++) acc[h][i] = 0.f;
-    for (int t = t0 + rr; t < t1; t += RPP) {
-        const u32x4 vw = *(const u32x4*)(a.vc + (size_t)t * a.kv_dim + col);
+    auto pv_row = [&](const u32x4 vw, const int t) {
         float vf[8];
         WDec<XH_F16>::dec(vw, vf);
 #pragma unroll
@@ -118,6 +152,24 @@ __global__ __launch_bounds__(ATTN_THREADS) void attn_split_kernel(const AttnArgs
             const float e = sc[h * T + (t - t0)];
 #pragma unroll
             for (int i = 0; i < 8; i++) acc[h][i] = fmaf(e, vf[i], acc[h][i]);
+        }
+    };
+#pragma unroll
+    for (int p = 0; p < ATTN_PREF; p++) {
+        const int t = t0 + rr + p * RPP;
+        if (t < t1) pv_row(vr[p], t);
+    }
+    for (int base = t0 + ATTN_PREF * RPP; base < t1; base += ATTN_PREF * RPP) {
+        u32x4 vv[ATTN_PREF];
+#pragma unroll
+        for (int p = 0; p < ATTN_PREF; p++) {
+            const int t = base + rr + p * RPP;
+            if (t < t1) vv[p] = *(const u32x4*)(a.vc + (size_t)t * a.kv_dim + col);
+        }
+#pragma unroll
+        for (int p = 0; p < ATTN_PREF; p++) {
+            const int t = base + rr + p * RPP;
+            if (t < t1) pv_row(vv[p], t);
         }
     }
     // reduce over the row slots of this wave (lanes sharing `sub`), then over waves
@@ -134,47 +186,68 @@ __global__ __launch_bounds__(ATTN_THREADS) void attn_split_kernel(const AttnArgs
             for (int i = 0; i < 8; i++) red[(wid * QPK + h) * HD + sub * 8 + i] = acc[h][i];
     }
     __syncthreads();
-    for (int idx = tid; idx < QPK * HD; idx += ATTN_THREADS) {
-        const int h = idx / HD;
-        const float o = red[idx] + red[QPK * HD + idx] + red[2 * QPK * HD + idx] + red[3 * QPK * HD + idx];
-        const int head = g * QPK + h;
-        const int d = idx - h * HD;
-        if (n_active == 1) {
-            a.out[(size_t)head * HD + d] = o / ml[2 * h + 1];
-        } else {
-            a.part_o[((size_t)s * a.n_heads + head) * HD + d] = o;
-            if (d == 0) {
-                a.part_ml[((size_t)s * a.n_heads + head) * 2] = ml[2 * h];
-                a.part_ml[((size_t)s * a.n_heads + head) * 2 + 1] = ml[2 * h + 1];
-            }
+    if (n_active == 1) {
+        for (int idx = tid; idx < QPK * HD; idx += ATTN_THREADS) {
+            const int h = idx / HD;
+            const float o = red[idx] + red[QPK * HD + idx] + red[2 * QPK * HD + idx] + red[3 * QPK * HD + idx];
+            a.out[(size_t)g * QPK * HD + idx] = o / ml[2 * h + 1];
         }
+        return;
     }
-}
 
-// merge split partials: out = sum_s e^{m_s-M} o_s / sum_s e^{m_s-M} l_s
-__global__ void attn_combine_kernel(const AttnArgs a, const int hd) {
-    const int kv_len = a.sp->kv_len;
-    const int T = attn_split_len(kv_len, a.nsplit);
-    const int n_active = (kv_len + T - 1) / T;
-    if (n_active <= 1) return;
-    const int head = blockIdx.x;
-    float M = -FLT_MAX;
-    for (int s = 0; s < n_active; s++) M = fmaxf(M, a.part_ml[((size_t)s * a.n_heads + head) * 2]);
-    for (int d = threadIdx.x; d < hd; d += blockDim.x) {
-        float num = 0.f, den = 0.f;
-        for (int s = 0; s < n_active; s++) {
-            const float* mlp = a.part_ml + ((size_t)s * a.n_heads + head) * 2;
+    // ---- partial store, then the last block of this KV head merges all splits ----
+    float* po = a.part_o + ((size_t)s * a.n_heads + g * QPK) * HD;
+    for (int idx = tid; idx < QPK * HD; idx += ATTN_THREADS)
+        po[idx] = red[idx] + red[QPK * HD + idx] + red[2 * QPK * HD + idx] + red[3 * QPK * HD + idx];
+    if (tid < 2 * QPK) a.part_ml[((size_t)s * a.n_heads + g * QPK) * 2 + tid] = ml[tid];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const int ticket = __hip_atomic_fetch_add(a.counters + g, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int last = ticket == n_active - 1;
+        if (last) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_store(a.counters + g, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        *flag = last;
+    }
+    __syncthreads();
+    if (!*flag) return;
+    // merge: out = sum_s e^{m_s-M} o_s / sum_s e^{m_s-M} l_s   (per head)
+    float* wts = sc;  // reuse: [QPK][n_active] weights, then [QPK] 1/den
+    for (int h = wid; h < QPK; h += ATTN_THREADS / 64) {
+        float M = -FLT_MAX;
+        for (int j = lane; j < n_active; j += 64)
+            M = fmaxf(M, a.part_ml[((size_t)j * a.n_heads + g * QPK + h) * 2]);
+        M = wave_max(M);
+        float den = 0.f;
+        for (int j = lane; j < n_active; j += 64) {
+            const float* mlp = a.part_ml + ((size_t)j * a.n_heads + g * QPK + h) * 2;
             const float f = expf(mlp[0] - M);
-            num = fmaf(f, a.part_o[((size_t)s * a.n_heads + head) * hd + d], num);
+            wts[h * n_active + j] = f;
             den = fmaf(f, mlp[1], den);
         }
-        a.out[(size_t)head * hd + d] = num / den;
+        den = wave_sum(den);
+        if (lane == 0) red[h] = den;
+    }
+    __syncthreads();
+    for (int idx = tid; idx < QPK * HD; idx += ATTN_THREADS) {
+        const int h = idx / HD;
+        const float* w = wts + h * n_active;
+        float num = 0.f;
+        for (int j = 0; j < n_active; j++)
+            num = fmaf(w[j], a.part_o[((size_t)j * a.n_heads + g * QPK) * HD + idx], num);
+        a.out[(size_t)g * QPK * HD + idx] = num / red[h];
     }
 }
 
 // shared-memory bytes of attn_split_kernel<HD,QPK> for a given max split length
-inline size_t attn_smem_bytes(const int hd, const int qpk, const int t_max) {
-    return sizeof(float) * (4 * qpk * hd + ((2 * qpk + 3) & ~3) + (size_t)qpk * t_max);
+inline size_t attn_smem_bytes(const int hd, const int qpk, const int t_max, const int nsplit) {
+    const size_t scn = (size_t)qpk * (t_max > nsplit ? t_max : nsplit);
+    return sizeof(float) * (4 * qpk * hd + ((2 * qpk + 4) & ~3) + scn);
 }
 
 }  // namespace xalm

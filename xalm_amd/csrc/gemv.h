@@ -24,7 +24,7 @@ namespace xalm {
 enum { PRO_PLAIN = 0, PRO_RMSNORM = 1 };
 enum { EPI_STORE = 0, EPI_RESID = 1, EPI_QKV = 2, EPI_GLU = 3 };
 
-constexpr int GEMV_THREADS = 256;
+constexpr int GEMV_THREADS = 512;
 constexpr int GEMV_WAVES = GEMV_THREADS / 64;
 constexpr int LDS_HEAD_BYTES = 64;  // block-reduction scratch in front of the x image
 
@@ -184,17 +184,23 @@ __device__ __forceinline__ void gemv_epilogue(const GemvArgs& a, const int row0,
     }
 }
 
-template <int DT, int ROWS, int U>
-__device__ __forceinline__ void gemv_chunk(const char* wrow, const size_t row_bytes, const float4* xs4, const int it,
-                                           const int lane, float* acc) {
-    constexpr int E = WDec<DT>::E;
-    constexpr int QN = E / 4;
-    u32x4 wv[U][ROWS];
+// Weight chunk `it` of a row group: U x ROWS 16-byte non-temporal loads per lane (1 KiB per
+// wave-instruction per row), straight to VGPRs.
+template <int ROWS, int U>
+__device__ __forceinline__ void gemv_load(u32x4 (&wv)[U][ROWS], const char* wrow, const size_t row_bytes,
+                                          const int it) {
 #pragma unroll
     for (int u = 0; u < U; u++)
 #pragma unroll
         for (int r = 0; r < ROWS; r++)
             wv[u][r] = __builtin_nontemporal_load((const u32x4*)(wrow + (size_t)r * row_bytes + (size_t)(it + u) * 1024));
+}
+
+template <int DT, int ROWS, int U>
+__device__ __forceinline__ void gemv_compute(const u32x4 (&wv)[U][ROWS], const float4* xs4, const int it,
+                                             const int lane, float* acc) {
+    constexpr int E = WDec<DT>::E;
+    constexpr int QN = E / 4;
 #pragma unroll
     for (int u = 0; u < U; u++) {
         float4 xv[QN];
@@ -217,6 +223,17 @@ __device__ __forceinline__ void gemv_chunk(const char* wrow, const size_t row_by
     }
 }
 
+template <int DT, int ROWS, int U>
+__device__ __forceinline__ void gemv_chunk(const char* wrow, const size_t row_bytes, const float4* xs4, const int it,
+                                           const int lane, float* acc) {
+    u32x4 wv[U][ROWS];
+    gemv_load<ROWS, U>(wv, wrow, row_bytes, it);
+    gemv_compute<DT, ROWS, U>(wv, xs4, it, lane, acc);
+}
+
+// Grid: every wave owns the same number of ROWS-row groups (g = wave, wave + W, ...), so no
+// wave is left with a partial last round.  The first U weight chunks of the first group are
+// requested before the x image is staged, so HBM latency overlaps the prologue.
 template <int DT, int PRO, int EPI, int ROWS, int U>
 __global__ __launch_bounds__(GEMV_THREADS) void gemv_kernel(const GemvArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -226,32 +243,55 @@ __global__ __launch_bounds__(GEMV_THREADS) void gemv_kernel(const GemvArgs a) {
     const int lane = threadIdx.x & 63;
     const int wid = threadIdx.x >> 6;
 
-    stage_x<E, PRO>(a, xs4, red);
-    if (EPI == EPI_QKV && blockIdx.x == 0) rotate_sinks(a, a.sp->kv_sink);
-    __syncthreads();
-
     const int n = a.n;
     const int n_full = n / (64 * E);
     const int n_it = (n + 64 * E - 1) / (64 * E);
     const int n_groups = (a.rows + ROWS - 1) / ROWS;
     const int total_waves = gridDim.x * GEMV_WAVES;
-    for (int g = blockIdx.x * GEMV_WAVES + wid; g < n_groups; g += total_waves) {
-        const int row0 = g * ROWS;
-        // rows past the end (odd vocab) re-read the last row and are never stored
-        const int rmax = a.rows - 1;
-        const size_t rb = a.row_bytes;
-        const char* wrow = (const char*)a.w + (size_t)(row0 < rmax ? row0 : rmax) * rb + lane * 16;
-        const size_t rstride = (row0 + ROWS - 1 <= rmax) ? rb : 0;
+    const int rmax = a.rows - 1;
+    const size_t rb = a.row_bytes;
+    int g = blockIdx.x * GEMV_WAVES + wid;
+
+    // rows past the end (odd vocab) re-read the last row and are never stored
+    auto row_ptr = [&](int grp, size_t& rstride) {
+        const int row0 = grp * ROWS;
+        rstride = (row0 + ROWS - 1 <= rmax) ? rb : 0;
+        return (const char*)a.w + (size_t)(row0 < rmax ? row0 : rmax) * rb + lane * 16;
+    };
+
+    u32x4 pre[U][ROWS];
+    const bool prefetched = g < n_groups && n_full >= U;
+    if (prefetched) {
+        size_t rs;
+        const char* wrow = row_ptr(g, rs);
+        gemv_load<ROWS, U>(pre, wrow, rs, 0);
+    }
+
+    stage_x<E, PRO>(a, xs4, red);
+    if (EPI == EPI_QKV && blockIdx.x == 0) rotate_sinks(a, a.sp->kv_sink);
+    __syncthreads();
+
+    bool first = prefetched;
+    for (; g < n_groups; g += total_waves) {
+        size_t rstride;
+        const char* wrow = row_ptr(g, rstride);
         float acc[ROWS];
 #pragma unroll
         for (int r = 0; r < ROWS; r++) acc[r] = 0.f;
         int it = 0;
+        if (first) {
+            gemv_compute<DT, ROWS, U>(pre, xs4, 0, lane, acc);
+            it = U;
+            first = false;
+        }
         for (; it + U <= n_full; it += U) gemv_chunk<DT, ROWS, U>(wrow, rstride, xs4, it, lane, acc);
-        for (; it < n_it; it++)
-            if ((it * 64 + lane) * E < n) gemv_chunk<DT, ROWS, 1>(wrow, rstride, xs4, it, lane, acc);
+        if (U > 4)
+            for (; it + 4 <= n_full; it += 4) gemv_chunk<DT, ROWS, (U > 4 ? 4 : 1)>(wrow, rstride, xs4, it, lane, acc);
+        for (; it < n_full; it++) gemv_chunk<DT, ROWS, 1>(wrow, rstride, xs4, it, lane, acc);
+        if (it < n_it && (it * 64 + lane) * E < n) gemv_chunk<DT, ROWS, 1>(wrow, rstride, xs4, it, lane, acc);
 #pragma unroll
         for (int r = 0; r < ROWS; r++) acc[r] = wave_sum(acc[r]);
-        if (lane == 0) gemv_epilogue<EPI, ROWS>(a, row0, acc);
+        if (lane == 0) gemv_epilogue<EPI, ROWS>(a, g * ROWS, acc);
     }
 }
 

@@ -10,7 +10,7 @@
 //   per layer:
 //     gemv<PRO_RMSNORM, EPI_QKV>    [Wq;Wk;Wv] (one fused matrix) + rmsnorm + clip + rope +
 //                                   fp16 K/V ring write + sink re-rotation
-//     attn_split_kernel / attn_combine_kernel      GQA attention over the ring
+//     attn_split_kernel             GQA attention over the ring (split-KV, in-kernel merge)
 //     gemv<PRO_PLAIN, EPI_RESID>    Wo, x += .
 //     gemv<PRO_RMSNORM, EPI_GLU>    [W1;W3] rows interleaved + rmsnorm + silu(g)*u
 //     gemv<PRO_PLAIN, EPI_RESID>    W2, x += .
@@ -49,7 +49,7 @@ bool matrix_dtype_ok(int dt) {
 int elems_per_16b(int dt) { return 16 / (int)dtype_size(dt); }
 
 constexpr int ROWS = 2;  // rows per wave (even: rope pairs, gate/up pairs)
-constexpr int UNROLL = 4;
+constexpr int UNROLL = 8;
 
 struct LayerW {
     void* wqkv = nullptr; int qkv_dt = 0; unsigned qkv_have = 0;  // bit0 q, bit1 k, bit2 v
@@ -75,6 +75,7 @@ struct xh_ctx {
     uint16_t* kv = nullptr;  // [n_layers][2][max_seq_len][kv_dim]
     float *x = nullptr, *q = nullptr, *attn_out = nullptr, *hb = nullptr, *logits = nullptr;
     float *part_o = nullptr, *part_ml = nullptr;
+    int* attn_cnt = nullptr;        // [n_kv_heads] split arrival tickets
     float *rope_freq = nullptr, *sink_cos = nullptr, *sink_sin = nullptr;
     StepParams* sp = nullptr;       // device
     StepParams* sp_host = nullptr;  // pinned
@@ -83,7 +84,7 @@ struct xh_ctx {
     int nsplit = 1, t_max = 16;
     bool use_graphs = true;
     hipGraphExec_t g_logits = nullptr, g_hydrate = nullptr, g_decode = nullptr;
-    int max_gemv_blocks = 1024;
+    int max_gemv_blocks = 512;  // 2 blocks of 8 waves per CU
 
     uint16_t* kcache(int l) { return kv + (size_t)l * 2 * c.max_seq_len * kv_dim; }
     uint16_t* vcache(int l) { return kcache(l) + (size_t)c.max_seq_len * kv_dim; }
@@ -117,9 +118,12 @@ void launch_gemv_t(const GemvArgs& a, hipStream_t s, int max_blocks) {
     constexpr int E = WDec<DT>::E;
     const int n_it = (a.n + 64 * E - 1) / (64 * E);
     const size_t smem = LDS_HEAD_BYTES + (size_t)n_it * 64 * E * sizeof(float);
+    // balanced rounds: at most max_blocks*GEMV_WAVES waves, each with the same group count
     const int n_groups = (a.rows + ROWS - 1) / ROWS;
-    int blocks = (n_groups + GEMV_WAVES - 1) / GEMV_WAVES;
-    if (blocks > max_blocks) blocks = max_blocks;
+    const int w_max = max_blocks * GEMV_WAVES;
+    const int rounds = (n_groups + w_max - 1) / w_max;
+    const int waves = (n_groups + rounds - 1) / rounds;
+    const int blocks = (waves + GEMV_WAVES - 1) / GEMV_WAVES;
     auto k = gemv_kernel<DT, PRO, EPI, ROWS, UNROLL>;
     if (smem > 64 * 1024) {
         static bool done = false;
@@ -149,7 +153,7 @@ bool launch_gemv(int dt, const GemvArgs& a, hipStream_t s, int max_blocks) {
 // ---------------------------------------------------------------------------------------
 template <int HD, int QPK>
 void launch_attn_t(const AttnArgs& a, int n_kv_heads, int t_max, hipStream_t s) {
-    const size_t smem = attn_smem_bytes(HD, QPK, t_max);
+    const size_t smem = attn_smem_bytes(HD, QPK, t_max, a.nsplit);
     auto k = attn_split_kernel<HD, QPK>;
     if (smem > 64 * 1024) {
         static bool done = false;
@@ -182,16 +186,12 @@ bool launch_attn(const AttnArgs& a, int hd, int qpk, int n_kv_heads, int t_max, 
         case 256: ok = launch_attn_hd<256>(a, qpk, n_kv_heads, t_max, s); break;
         default: return false;
     }
-    if (ok && a.nsplit > 1) {
-        const int thr = hd < 64 ? 64 : hd;
-        hipLaunchKernelGGL(attn_combine_kernel, dim3(a.n_heads), dim3(thr), 0, s, a, hd);
-    }
     return ok;
 }
 
 int attn_nsplit(int n_kv_heads, int max_seq_len) {
     int ns = 512 / n_kv_heads;
-    const int cap = (max_seq_len + 15) / 16;
+    const int cap = (max_seq_len + ATTN_MIN_T - 1) / ATTN_MIN_T;
     if (ns > cap) ns = cap;
     return ns < 1 ? 1 : ns;
 }
@@ -246,7 +246,7 @@ AttnArgs attn_args(xh_ctx* ctx, int l) {
     AttnArgs a{};
     a.q = ctx->q; a.kc = ctx->kcache(l); a.vc = ctx->vcache(l); a.kv_dim = ctx->kv_dim;
     a.n_heads = ctx->c.n_heads; a.nsplit = ctx->nsplit; a.out = ctx->attn_out;
-    a.part_o = ctx->part_o; a.part_ml = ctx->part_ml; a.sp = ctx->sp;
+    a.part_o = ctx->part_o; a.part_ml = ctx->part_ml; a.counters = ctx->attn_cnt; a.sp = ctx->sp;
     return a;
 }
 
@@ -437,6 +437,7 @@ int xh_create(const xh_config* cfg, int device_ordinal, xh_ctx** out) {
     CREATE_TRY(dmalloc(ctx, &ctx->logits, (size_t)c.vocab_size));
     CREATE_TRY(dmalloc(ctx, &ctx->part_o, (size_t)ctx->nsplit * ctx->q_dim));
     CREATE_TRY(dmalloc(ctx, &ctx->part_ml, (size_t)ctx->nsplit * c.n_heads * 2));
+    CREATE_TRY(dmalloc(ctx, &ctx->attn_cnt, (size_t)c.n_kv_heads));
     CREATE_TRY(dmalloc(ctx, &ctx->rope_freq, (size_t)c.head_dim / 2));
     CREATE_TRY(dmalloc(ctx, &ctx->sink_cos, (size_t)c.head_dim / 2));
     CREATE_TRY(dmalloc(ctx, &ctx->sink_sin, (size_t)c.head_dim / 2));
@@ -483,7 +484,7 @@ void xh_destroy(xh_ctx* ctx) {
     if (ctx->wcls && ctx->wcls != ctx->embed) hipFree(ctx->wcls);
     hipFree(ctx->embed); hipFree(ctx->final_norm);
     hipFree(ctx->kv); hipFree(ctx->x); hipFree(ctx->q); hipFree(ctx->attn_out); hipFree(ctx->hb);
-    hipFree(ctx->logits); hipFree(ctx->part_o); hipFree(ctx->part_ml); hipFree(ctx->rope_freq);
+    hipFree(ctx->logits); hipFree(ctx->part_o); hipFree(ctx->part_ml); hipFree(ctx->attn_cnt); hipFree(ctx->rope_freq);
     hipFree(ctx->sink_cos); hipFree(ctx->sink_sin); hipFree(ctx->sp); hipFree(ctx->dec_tokens);
     if (ctx->sp_host) hipHostFree(ctx->sp_host);
     if (ctx->stream) hipStreamDestroy(ctx->stream);
@@ -863,7 +864,8 @@ int xh_op_mha(float* xout, const uint16_t* kb, const uint16_t* vb, const float* 
     const int qpk = n_heads / n_kv_heads, kv_dim = n_kv_heads * head_dim;
     const int nsplit = attn_nsplit(n_kv_heads, max_seq_len);
     const int t_max = attn_split_len(max_seq_len, nsplit);
-    DevBuf bk, bv, bq, bo, bpo, bpm, bsp;
+    DevBuf bk, bv, bq, bo, bpo, bpm, bsp, bcnt;
+    std::vector<int> zeros((size_t)n_kv_heads, 0);
     StepParams sp{};
     sp.kv_len = kv_len;
     sp.max_seq_len = max_seq_len;
@@ -872,12 +874,13 @@ int xh_op_mha(float* xout, const uint16_t* kb, const uint16_t* vb, const float* 
     if ((rc = op_alloc(bk, kvb, kb)) || (rc = op_alloc(bv, kvb, vb)) || (rc = op_alloc(bq, (size_t)n_heads * head_dim * 4, q)) ||
         (rc = op_alloc(bo, (size_t)n_heads * head_dim * 4, nullptr)) ||
         (rc = op_alloc(bpo, (size_t)nsplit * n_heads * head_dim * 4, nullptr)) ||
-        (rc = op_alloc(bpm, (size_t)nsplit * n_heads * 2 * 4, nullptr)) || (rc = op_alloc(bsp, sizeof sp, &sp)))
+        (rc = op_alloc(bpm, (size_t)nsplit * n_heads * 2 * 4, nullptr)) || (rc = op_alloc(bsp, sizeof sp, &sp)) ||
+        (rc = op_alloc(bcnt, zeros.size() * sizeof(int), zeros.data())))
         return rc;
     AttnArgs a{};
     a.q = (const float*)bq.p; a.kc = (const uint16_t*)bk.p; a.vc = (const uint16_t*)bv.p; a.kv_dim = kv_dim;
     a.n_heads = n_heads; a.nsplit = nsplit; a.out = (float*)bo.p; a.part_o = (float*)bpo.p;
-    a.part_ml = (float*)bpm.p; a.sp = (const StepParams*)bsp.p;
+    a.part_ml = (float*)bpm.p; a.counters = (int*)bcnt.p; a.sp = (const StepParams*)bsp.p;
     if (!launch_attn(a, head_dim, qpk, n_kv_heads, t_max, nullptr))
         return set_err(nullptr, XH_E_INVALID, "unsupported head_dim %d / qpk %d", head_dim, qpk);
     return op_finish(xout, bo, (size_t)n_heads * head_dim * 4);
