@@ -1,0 +1,127 @@
+// gemv_bench.hip — one-process A/B of gemv launch shapes on the Mistral-7B f16 matrix shapes.
+// Build: hipcc -O3 --offload-arch=gfx950 -std=c++17 -o tools/gemv_bench tools/gemv_bench.hip
+// Each shape rotates over enough weight copies (> 1 GB) that the 256 MB Infinity Cache
+// cannot serve repeats; variants are interleaved over rounds (guide §5.4 rule 24).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <functional>
+#include <string>
+#include <vector>
+
+#include "../include/xalm_synth.h"
+#include "../xalm_amd/csrc/gemv.h"
+
+using namespace xalm;
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s @%d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
+
+__global__ void fill(uint16_t* p, size_t n, uint64_t seed) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+        p[i] = xs_to_f16(xs_value(seed, i, 0.f, 0.02f));
+}
+__global__ void fillf(float* p, size_t n, uint64_t seed) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+        p[i] = xs_value(seed, i, 0.f, 1.f);
+}
+
+struct Mat { const char* name; int rows, n, pro, epi; };
+
+template <int PRO, int EPI, class S>
+void launch(const GemvArgs& a, int max_waves) {
+    const size_t smem = gemv_smem_bytes<XH_F16, S>(a.n);
+    const int blocks = gemv_blocks<S>(a.rows, max_waves / S::WAVES);
+    auto k = gemv_kernel<XH_F16, PRO, EPI, S>;
+    static bool once = false;
+    if (!once) { CK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024)); once = true; }
+    hipLaunchKernelGGL(k, dim3(blocks), dim3(S::THREADS), smem, 0, a);
+}
+
+template <class S>
+void launch_any(const Mat& m, const GemvArgs& a, int mw) {
+    if (m.pro == PRO_RMSNORM && m.epi == EPI_GLU) launch<PRO_RMSNORM, EPI_GLU, S>(a, mw);
+    else if (m.pro == PRO_RMSNORM) launch<PRO_RMSNORM, EPI_STORE, S>(a, mw);
+    else launch<PRO_PLAIN, EPI_RESID, S>(a, mw);
+}
+
+struct Variant { std::string name; std::function<void(const Mat&, const GemvArgs&)> fn; };
+
+int main(int argc, char** argv) {
+    const int iters = argc > 1 ? atoi(argv[1]) : 40;
+    const int rounds = argc > 2 ? atoi(argv[2]) : 3;
+    std::vector<Mat> mats = {{"w13 28672x4096", 28672, 4096, PRO_RMSNORM, EPI_GLU},
+                             {"w2 4096x14336", 4096, 14336, PRO_PLAIN, EPI_RESID},
+                             {"qkv 6144x4096", 6144, 4096, PRO_RMSNORM, EPI_STORE},
+                             {"wo 4096x4096", 4096, 4096, PRO_PLAIN, EPI_RESID},
+                             {"cls 32000x4096", 32000, 4096, PRO_RMSNORM, EPI_STORE}};
+    float *x, *out, *nw;
+    CK(hipMalloc(&x, 14336 * 4));
+    CK(hipMalloc(&out, 32000 * 4));
+    CK(hipMalloc(&nw, 14336 * 4));
+    hipLaunchKernelGGL(fillf, dim3(64), dim3(256), 0, 0, x, 14336, 7);
+    hipLaunchKernelGGL(fillf, dim3(64), dim3(256), 0, 0, nw, 14336, 8);
+    std::vector<std::vector<uint16_t*>> copies(mats.size());
+    for (size_t i = 0; i < mats.size(); i++) {
+        const size_t elems = (size_t)mats[i].rows * mats[i].n;
+        const int nc = std::max<int>(2, (int)((1400ull << 20) / (elems * 2)) + 1);
+        for (int c = 0; c < nc; c++) {
+            uint16_t* p;
+            CK(hipMalloc(&p, elems * 2));
+            hipLaunchKernelGGL(fill, dim3(2048), dim3(256), 0, 0, p, elems, 100 + i * 10 + c);
+            copies[i].push_back(p);
+        }
+    }
+    CK(hipDeviceSynchronize());
+
+#define V(NAME, MW, ...) {NAME, [](const Mat& m, const GemvArgs& a) { launch_any<GemvShape<__VA_ARGS__>>(m, a, MW); }}
+    std::vector<Variant> vs = {
+        V("t256 r2 u4 nt pf  w4096", 4096, 256, 2, 4, true, 4, true),
+        V("t256 r2 u4 nt --  w4096", 4096, 256, 2, 4, true, 4, false),
+        V("t256 r2 u2 nt pf  w4096", 4096, 256, 2, 2, true, 4, true),
+        V("t256 r2 u2 nt --  w4096", 4096, 256, 2, 2, true, 4, false),
+        V("t256 r4 u2 nt --  w4096", 4096, 256, 4, 2, true, 4, false),
+        V("t256 r2 u4 -- --  w4096", 4096, 256, 2, 4, false, 4, false),
+        V("t256 r2 u8 nt --  w2048 mw2", 2048, 256, 2, 8, true, 2, false),
+        V("t256 r2 u4 nt --  w2048", 2048, 256, 2, 4, true, 4, false),
+        V("t256 r2 u4 nt --  w8192 mw8", 8192, 256, 2, 4, true, 8, false),
+        V("t512 r2 u4 nt --  w4096", 4096, 512, 2, 4, true, 4, false),
+        V("t512 r2 u2 nt pf  w4096", 4096, 512, 2, 2, true, 4, true),
+        V("t128 r2 u4 nt --  w4096", 4096, 128, 2, 4, true, 4, false),
+    };
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    // results[mat][variant] = list of us
+    std::vector<std::vector<std::vector<float>>> res(mats.size(), std::vector<std::vector<float>>(vs.size()));
+    for (int r = 0; r < rounds; r++)
+        for (size_t mi = 0; mi < mats.size(); mi++)
+            for (size_t vi = 0; vi < vs.size(); vi++) {
+                const Mat& m = mats[mi];
+                if (m.n > 8192 && std::string(vs[vi].name).find("t128") == 0) continue;
+                GemvArgs a{};
+                a.row_bytes = (size_t)m.n * 2; a.n = m.n; a.rows = m.rows; a.x = x; a.norm_w = nw;
+                a.norm_dtype = XH_F32; a.eps = 1e-5f; a.out = out; a.act = XH_ACT_SILU;
+                for (int i = 0; i < 2; i++) { a.w = copies[mi][i % copies[mi].size()]; vs[vi].fn(m, a); }
+                CK(hipEventRecord(e0, 0));
+                for (int i = 0; i < iters; i++) { a.w = copies[mi][i % copies[mi].size()]; vs[vi].fn(m, a); }
+                CK(hipEventRecord(e1, 0));
+                CK(hipEventSynchronize(e1));
+                float ms;
+                CK(hipEventElapsedTime(&ms, e0, e1));
+                CK(hipGetLastError());
+                res[mi][vi].push_back(ms * 1000.f / iters);
+            }
+    for (size_t mi = 0; mi < mats.size(); mi++) {
+        const double bytes = (double)mats[mi].rows * mats[mi].n * 2;
+        printf("%s  (%.1f MB)\n", mats[mi].name, bytes / 1e6);
+        for (size_t vi = 0; vi < vs.size(); vi++) {
+            auto v = res[mi][vi];
+            if (v.empty()) continue;
+            std::sort(v.begin(), v.end());
+            printf("   %-28s median %8.2f us  min %8.2f  -> %7.1f GB/s\n", vs[vi].name.c_str(), v[v.size() / 2], v[0],
+                   bytes / (v[v.size() / 2] * 1e-6) / 1e9);
+        }
+    }
+    return 0;
+}

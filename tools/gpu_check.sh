@@ -25,6 +25,7 @@ for s in $STEPS; do
         bench_f8) run bench_f8 600 python bench.py --workload mistral-7b-f8 ;;
         bench_32k) run bench_32k 600 python bench.py --workload mistral-7b-f16-32k --steps 64 ;;
         bench_llama) run bench_llama 600 python bench.py --workload llama3-8b-f16 ;;
+        gemvbench) run gemvbench 300 ./tools/gemv_bench 40 3 ;;
         prof) run prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
                   python bench.py --steps 64 --warmup 4 --no-cpu-baseline --kernel-iters 50 ;;
     esac

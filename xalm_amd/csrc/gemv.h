@@ -10,11 +10,11 @@
 //
 // HBM layout: W row-major [rows][n] exactly as the .xalm tensor (HF [out,in]).  One wave
 // owns ROWS consecutive rows; lane l streams 16-byte chunks l, l+64, l+128, ... of each row
-// (1 KiB per wave-instruction per row, fully coalesced) with non-temporal loads (weights are
-// read once per token).  The activation vector is staged once per workgroup in LDS in a
-// lane-permuted layout so every lane reads its matching x values with conflict-free
-// ds_read_b128.  Dot products reduce across the wave with cross-lane shuffles; there is no
-// MFMA: batch-1 matvec is HBM-bound at ~1 FLOP per weight byte.
+// (1 KiB per wave-instruction per row, fully coalesced), U chunks per row in flight, with
+// non-temporal loads (weights are read once per token).  The activation vector is staged once
+// per workgroup in LDS in a lane-permuted layout so every lane reads its x values with
+// conflict-free ds_read_b128.  Dot products reduce across the wave with cross-lane shuffles;
+// no MFMA: batch-1 matvec is HBM-bound at ~1 FLOP per weight byte.
 #pragma once
 
 #include "common.h"
@@ -24,9 +24,19 @@ namespace xalm {
 enum { PRO_PLAIN = 0, PRO_RMSNORM = 1 };
 enum { EPI_STORE = 0, EPI_RESID = 1, EPI_QKV = 2, EPI_GLU = 3 };
 
-constexpr int GEMV_THREADS = 512;
-constexpr int GEMV_WAVES = GEMV_THREADS / 64;
 constexpr int LDS_HEAD_BYTES = 64;  // block-reduction scratch in front of the x image
+
+// Launch shape of one gemv instance.
+template <int THREADS_, int ROWS_, int U_, bool NT_ = true, int MINW_ = 4, bool PF_ = true>
+struct GemvShape {
+    static constexpr int THREADS = THREADS_;   // workgroup size
+    static constexpr int WAVES = THREADS_ / 64;
+    static constexpr int ROWS = ROWS_;         // rows per wave and group (even for QKV / GLU)
+    static constexpr int U = U_;               // 16-B chunks per row in flight
+    static constexpr bool NT = NT_;            // non-temporal weight loads
+    static constexpr int MINW = MINW_;         // __launch_bounds__ min waves per SIMD
+    static constexpr bool PF = PF_;            // first chunk requested before the x prologue
+};
 
 struct GemvArgs {
     const void* w;        // [rows][n]
@@ -74,13 +84,14 @@ __device__ __forceinline__ void rope_pair(float& v0, float& v1, const int i, con
     v1 = a * fci + b * fcr;
 }
 
-// Sum of squares of x[0..n) -> rms scale 1/sqrtf(ss/n + eps), identical in every block
-// (fixed per-thread stride order, fixed shuffle tree, fixed wave order).
+// Sum of squares of x[0..n) -> rms scale 1/sqrtf(ss/n + eps), identical in every block of one
+// launch (fixed per-thread stride order, fixed shuffle tree, fixed wave order).
+template <int THREADS>
 __device__ __forceinline__ float block_rms_scale(const float* x, const int n, const float eps, float* red) {
     const int tid = threadIdx.x;
     const float4* x4 = (const float4*)x;
     float ss = 0.f;
-    for (int i = tid; i < (n >> 2); i += GEMV_THREADS) {
+    for (int i = tid; i < (n >> 2); i += THREADS) {
         const float4 v = x4[i];
         ss += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
     }
@@ -89,7 +100,7 @@ __device__ __forceinline__ float block_rms_scale(const float* x, const int n, co
     __syncthreads();
     float tot = 0.f;
 #pragma unroll
-    for (int w = 0; w < GEMV_WAVES; w++) tot += red[w];
+    for (int w = 0; w < THREADS / 64; w++) tot += red[w];
     const float rms = sqrtf(tot / (float)n + eps);
     return 1.0f / rms;
 }
@@ -105,13 +116,13 @@ __device__ __forceinline__ float4 load_norm4(const void* w, const int dtype, con
 
 // x (optionally rms-normalised and weighted) -> LDS image xs4, permuted so that lane l at
 // chunk `it` finds the E/4 float4 it multiplies at xs4[(it*E/4 + q)*64 + l].
-template <int E, int PRO>
+template <int E, int PRO, int THREADS>
 __device__ __forceinline__ void stage_x(const GemvArgs& a, float4* xs4, float* red) {
     const int n = a.n;
     float scale = 1.f;
-    if (PRO == PRO_RMSNORM) scale = block_rms_scale(a.x, n, a.eps, red);
+    if (PRO == PRO_RMSNORM) scale = block_rms_scale<THREADS>(a.x, n, a.eps, red);
     const float4* x4 = (const float4*)a.x;
-    for (int i = threadIdx.x; i < (n >> 2); i += GEMV_THREADS) {
+    for (int i = threadIdx.x; i < (n >> 2); i += THREADS) {
         float4 v = x4[i];
         if (PRO == PRO_RMSNORM) {
             const float4 w = load_norm4(a.norm_w, a.norm_dtype, i);
@@ -130,10 +141,11 @@ __device__ __forceinline__ void stage_x(const GemvArgs& a, float4* xs4, float* r
 }
 
 // StreamingLLM sink re-rotation (src/infer.cpp:421-431): K[r] = f16(rope(f32(K[r]), pos=1)).
+template <int THREADS>
 __device__ __forceinline__ void rotate_sinks(const GemvArgs& a, const int kv_sink) {
     for (int r = 0; r < kv_sink; r++) {
         uint16_t* krow = a.kcache + (size_t)r * a.kv_dim;
-        for (int p = threadIdx.x; p < (a.kv_dim >> 1); p += GEMV_THREADS) {
+        for (int p = threadIdx.x; p < (a.kv_dim >> 1); p += THREADS) {
             const int i = p << 1;
             const int jh = (i % a.head_dim) >> 1;
             const float k0 = f16_bits_to_f32(krow[i]), k1 = f16_bits_to_f32(krow[i + 1]);
@@ -184,16 +196,17 @@ __device__ __forceinline__ void gemv_epilogue(const GemvArgs& a, const int row0,
     }
 }
 
-// Weight chunk `it` of a row group: U x ROWS 16-byte non-temporal loads per lane (1 KiB per
-// wave-instruction per row), straight to VGPRs.
-template <int ROWS, int U>
+// Weight chunks [it, it+U) of a row group: U x ROWS 16-byte loads per lane, straight to VGPRs.
+template <int ROWS, int U, bool NT>
 __device__ __forceinline__ void gemv_load(u32x4 (&wv)[U][ROWS], const char* wrow, const size_t row_bytes,
                                           const int it) {
 #pragma unroll
     for (int u = 0; u < U; u++)
 #pragma unroll
-        for (int r = 0; r < ROWS; r++)
-            wv[u][r] = __builtin_nontemporal_load((const u32x4*)(wrow + (size_t)r * row_bytes + (size_t)(it + u) * 1024));
+        for (int r = 0; r < ROWS; r++) {
+            const u32x4* p = (const u32x4*)(wrow + (size_t)r * row_bytes + (size_t)(it + u) * 1024);
+            wv[u][r] = NT ? __builtin_nontemporal_load(p) : *p;
+        }
 }
 
 template <int DT, int ROWS, int U>
@@ -223,19 +236,20 @@ __device__ __forceinline__ void gemv_compute(const u32x4 (&wv)[U][ROWS], const f
     }
 }
 
-template <int DT, int ROWS, int U>
+template <int DT, int ROWS, int U, bool NT>
 __device__ __forceinline__ void gemv_chunk(const char* wrow, const size_t row_bytes, const float4* xs4, const int it,
                                            const int lane, float* acc) {
     u32x4 wv[U][ROWS];
-    gemv_load<ROWS, U>(wv, wrow, row_bytes, it);
+    gemv_load<ROWS, U, NT>(wv, wrow, row_bytes, it);
     gemv_compute<DT, ROWS, U>(wv, xs4, it, lane, acc);
 }
 
 // Grid: every wave owns the same number of ROWS-row groups (g = wave, wave + W, ...), so no
 // wave is left with a partial last round.  The first U weight chunks of the first group are
 // requested before the x image is staged, so HBM latency overlaps the prologue.
-template <int DT, int PRO, int EPI, int ROWS, int U>
-__global__ __launch_bounds__(GEMV_THREADS) void gemv_kernel(const GemvArgs a) {
+template <int DT, int PRO, int EPI, class S>
+__global__ __launch_bounds__(S::THREADS, S::MINW) void gemv_kernel(const GemvArgs a) {
+    constexpr int ROWS = S::ROWS, U = S::U;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     float* red = (float*)smem;
     float4* xs4 = (float4*)(smem + LDS_HEAD_BYTES);
@@ -247,10 +261,10 @@ __global__ __launch_bounds__(GEMV_THREADS) void gemv_kernel(const GemvArgs a) {
     const int n_full = n / (64 * E);
     const int n_it = (n + 64 * E - 1) / (64 * E);
     const int n_groups = (a.rows + ROWS - 1) / ROWS;
-    const int total_waves = gridDim.x * GEMV_WAVES;
+    const int total_waves = gridDim.x * S::WAVES;
     const int rmax = a.rows - 1;
     const size_t rb = a.row_bytes;
-    int g = blockIdx.x * GEMV_WAVES + wid;
+    int g = blockIdx.x * S::WAVES + wid;
 
     // rows past the end (odd vocab) re-read the last row and are never stored
     auto row_ptr = [&](int grp, size_t& rstride) {
@@ -260,15 +274,15 @@ __global__ __launch_bounds__(GEMV_THREADS) void gemv_kernel(const GemvArgs a) {
     };
 
     u32x4 pre[U][ROWS];
-    const bool prefetched = g < n_groups && n_full >= U;
+    const bool prefetched = S::PF && g < n_groups && n_full >= U;
     if (prefetched) {
         size_t rs;
         const char* wrow = row_ptr(g, rs);
-        gemv_load<ROWS, U>(pre, wrow, rs, 0);
+        gemv_load<ROWS, U, S::NT>(pre, wrow, rs, 0);
     }
 
-    stage_x<E, PRO>(a, xs4, red);
-    if (EPI == EPI_QKV && blockIdx.x == 0) rotate_sinks(a, a.sp->kv_sink);
+    stage_x<E, PRO, S::THREADS>(a, xs4, red);
+    if (EPI == EPI_QKV && blockIdx.x == 0) rotate_sinks<S::THREADS>(a, a.sp->kv_sink);
     __syncthreads();
 
     bool first = prefetched;
@@ -284,23 +298,40 @@ __global__ __launch_bounds__(GEMV_THREADS) void gemv_kernel(const GemvArgs a) {
             it = U;
             first = false;
         }
-        for (; it + U <= n_full; it += U) gemv_chunk<DT, ROWS, U>(wrow, rstride, xs4, it, lane, acc);
-        if (U > 4)
-            for (; it + 4 <= n_full; it += 4) gemv_chunk<DT, ROWS, (U > 4 ? 4 : 1)>(wrow, rstride, xs4, it, lane, acc);
-        for (; it < n_full; it++) gemv_chunk<DT, ROWS, 1>(wrow, rstride, xs4, it, lane, acc);
-        if (it < n_it && (it * 64 + lane) * E < n) gemv_chunk<DT, ROWS, 1>(wrow, rstride, xs4, it, lane, acc);
+        for (; it + U <= n_full; it += U) gemv_chunk<DT, ROWS, U, S::NT>(wrow, rstride, xs4, it, lane, acc);
+        if (U > 2)
+            for (; it + 2 <= n_full; it += 2) gemv_chunk<DT, ROWS, 2, S::NT>(wrow, rstride, xs4, it, lane, acc);
+        for (; it < n_full; it++) gemv_chunk<DT, ROWS, 1, S::NT>(wrow, rstride, xs4, it, lane, acc);
+        if (it < n_it && (it * 64 + lane) * E < n) gemv_chunk<DT, ROWS, 1, S::NT>(wrow, rstride, xs4, it, lane, acc);
 #pragma unroll
         for (int r = 0; r < ROWS; r++) acc[r] = wave_sum(acc[r]);
         if (lane == 0) gemv_epilogue<EPI, ROWS>(a, g * ROWS, acc);
     }
 }
 
+// LDS bytes and grid of one launch
+template <int DT, class S>
+inline size_t gemv_smem_bytes(const int n) {
+    constexpr int E = WDec<DT>::E;
+    const int n_it = (n + 64 * E - 1) / (64 * E);
+    return LDS_HEAD_BYTES + (size_t)n_it * 64 * E * sizeof(float);
+}
+// balanced rounds: at most max_blocks * WAVES waves, each with the same group count
+template <class S>
+inline int gemv_blocks(const int rows, const int max_blocks) {
+    const int n_groups = (rows + S::ROWS - 1) / S::ROWS;
+    const int w_max = max_blocks * S::WAVES;
+    const int rounds = (n_groups + w_max - 1) / w_max;
+    const int waves = (n_groups + rounds - 1) / rounds;
+    return (waves + S::WAVES - 1) / S::WAVES;
+}
+
 // rmsnorm as a standalone op (xh_op_rmsnorm), same reduction as the fused prologue.
-__global__ __launch_bounds__(GEMV_THREADS) void rmsnorm_kernel(float* o, const float* x, const void* w, int dtype,
-                                                                 int n, float eps) {
-    __shared__ float red[GEMV_WAVES];
-    const float scale = block_rms_scale(x, n, eps, red);
-    for (int i = threadIdx.x; i < (n >> 2); i += GEMV_THREADS) {
+__global__ __launch_bounds__(256) void rmsnorm_kernel(float* o, const float* x, const void* w, int dtype, int n,
+                                                       float eps) {
+    __shared__ float red[4];
+    const float scale = block_rms_scale<256>(x, n, eps, red);
+    for (int i = threadIdx.x; i < (n >> 2); i += 256) {
         const float4 v = ((const float4*)x)[i];
         const float4 wv = load_norm4(w, dtype, i);
         ((float4*)o)[i] = make_float4(v.x * scale * wv.x, v.y * scale * wv.y, v.z * scale * wv.z, v.w * scale * wv.w);
@@ -310,7 +341,7 @@ __global__ __launch_bounds__(GEMV_THREADS) void rmsnorm_kernel(float* o, const f
 // rope as a standalone op (xh_op_rope), same device function as the QKV epilogue.
 __global__ void rope_kernel(float* vec, int d, int head_dim, int pos, const float* freq) {
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (2 * p + 1 >= d + 1) return;
+    if (2 * p >= d) return;
     float v0 = vec[2 * p], v1 = vec[2 * p + 1];
     rope_pair(v0, v1, 2 * p, head_dim, pos, freq);
     vec[2 * p] = v0;

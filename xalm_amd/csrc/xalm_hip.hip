@@ -49,7 +49,7 @@ bool matrix_dtype_ok(int dt) {
 int elems_per_16b(int dt) { return 16 / (int)dtype_size(dt); }
 
 constexpr int ROWS = 2;  // rows per wave (even: rope pairs, gate/up pairs)
-constexpr int UNROLL = 8;
+constexpr int UNROLL = 4;
 
 struct LayerW {
     void* wqkv = nullptr; int qkv_dt = 0; unsigned qkv_have = 0;  // bit0 q, bit1 k, bit2 v
@@ -84,7 +84,7 @@ struct xh_ctx {
     int nsplit = 1, t_max = 16;
     bool use_graphs = true;
     hipGraphExec_t g_logits = nullptr, g_hydrate = nullptr, g_decode = nullptr;
-    int max_gemv_blocks = 512;  // 2 blocks of 8 waves per CU
+    int max_gemv_waves = 4096;  // 16 waves per CU
 
     uint16_t* kcache(int l) { return kv + (size_t)l * 2 * c.max_seq_len * kv_dim; }
     uint16_t* vcache(int l) { return kcache(l) + (size_t)c.max_seq_len * kv_dim; }
@@ -113,18 +113,16 @@ int set_err(xh_ctx* ctx, int code, const char* fmt, ...) {
 // ---------------------------------------------------------------------------------------
 // gemv launch dispatch
 // ---------------------------------------------------------------------------------------
-template <int DT, int PRO, int EPI>
-void launch_gemv_t(const GemvArgs& a, hipStream_t s, int max_blocks) {
-    constexpr int E = WDec<DT>::E;
-    const int n_it = (a.n + 64 * E - 1) / (64 * E);
-    const size_t smem = LDS_HEAD_BYTES + (size_t)n_it * 64 * E * sizeof(float);
-    // balanced rounds: at most max_blocks*GEMV_WAVES waves, each with the same group count
-    const int n_groups = (a.rows + ROWS - 1) / ROWS;
-    const int w_max = max_blocks * GEMV_WAVES;
-    const int rounds = (n_groups + w_max - 1) / w_max;
-    const int waves = (n_groups + rounds - 1) / rounds;
-    const int blocks = (waves + GEMV_WAVES - 1) / GEMV_WAVES;
-    auto k = gemv_kernel<DT, PRO, EPI, ROWS, UNROLL>;
+// Shapes (tools/gemv_bench.hip measures the alternatives): short rows (x image <= 40 KB, all
+// of Mistral's matrices but W2) use 256-thread blocks, long rows share one x image over 512.
+using ShapeShort = GemvShape<256, ROWS, UNROLL, true, 4>;
+using ShapeLong = GemvShape<512, ROWS, UNROLL, true, 4>;
+
+template <int DT, int PRO, int EPI, class S>
+void launch_gemv_s(const GemvArgs& a, hipStream_t s, int max_waves) {
+    const size_t smem = gemv_smem_bytes<DT, S>(a.n);
+    const int blocks = gemv_blocks<S>(a.rows, max_waves / S::WAVES);
+    auto k = gemv_kernel<DT, PRO, EPI, S>;
     if (smem > 64 * 1024) {
         static bool done = false;
         if (!done) {
@@ -132,7 +130,13 @@ void launch_gemv_t(const GemvArgs& a, hipStream_t s, int max_blocks) {
             done = true;
         }
     }
-    hipLaunchKernelGGL(k, dim3(blocks), dim3(GEMV_THREADS), smem, s, a);
+    hipLaunchKernelGGL(k, dim3(blocks), dim3(S::THREADS), smem, s, a);
+}
+
+template <int DT, int PRO, int EPI>
+void launch_gemv_t(const GemvArgs& a, hipStream_t s, int max_waves) {
+    if (gemv_smem_bytes<DT, ShapeShort>(a.n) <= 40 * 1024) launch_gemv_s<DT, PRO, EPI, ShapeShort>(a, s, max_waves);
+    else launch_gemv_s<DT, PRO, EPI, ShapeLong>(a, s, max_waves);
 }
 
 template <int PRO, int EPI>
@@ -283,7 +287,7 @@ __global__ void argmax_advance_kernel(const float* logits, int vocab, StepParams
 
 int enqueue_step(xh_ctx* ctx, hipStream_t s, bool with_logits) {
     const xh_config& c = ctx->c;
-    const int mb = ctx->max_gemv_blocks;
+    const int mb = ctx->max_gemv_waves;
     hipLaunchKernelGGL(embed_kernel, dim3((c.dim + 255) / 256), dim3(256), 0, s, (const void*)ctx->embed,
                        ctx->embed_dt, c.dim, ctx->x, (const StepParams*)ctx->sp);
     for (int l = 0; l < c.n_layers; l++) {
@@ -827,7 +831,7 @@ int xh_op_matmul(float* xout, const float* x, const void* w, int dtype, int n, i
     GemvArgs a{};
     a.w = bw.p; a.row_bytes = (size_t)n * dtype_size(dtype); a.n = n; a.rows = d;
     a.x = (const float*)bx.p; a.out = (float*)bo.p;
-    launch_gemv<PRO_PLAIN, EPI_STORE>(dtype, a, nullptr, 1024);
+    launch_gemv<PRO_PLAIN, EPI_STORE>(dtype, a, nullptr, 4096);
     return op_finish(xout, bo, (size_t)d * 4);
 }
 
@@ -839,7 +843,7 @@ int xh_op_rmsnorm(float* o, const float* x, const void* weight, int dtype, int s
     if ((rc = op_alloc(bw, (size_t)size * dtype_size(dtype), weight)) || (rc = op_alloc(bx, (size_t)size * 4, x)) ||
         (rc = op_alloc(bo, (size_t)size * 4, nullptr)))
         return rc;
-    hipLaunchKernelGGL(rmsnorm_kernel, dim3(1), dim3(GEMV_THREADS), 0, nullptr, (float*)bo.p, (const float*)bx.p,
+    hipLaunchKernelGGL(rmsnorm_kernel, dim3(1), dim3(256), 0, nullptr, (float*)bo.p, (const float*)bx.p,
                        (const void*)bw.p, dtype, size, eps);
     return op_finish(o, bo, (size_t)size * 4);
 }
@@ -894,16 +898,20 @@ int xh_time_kernel(xh_ctx* ctx, int which, int iters, float* avg_us) {
     HIP_TRY(ctx, hipSetDevice(ctx->dev));
     int rc = check_ready(ctx);
     if (rc) return rc;
-    const int mb = ctx->max_gemv_blocks;
+    const int mb = ctx->max_gemv_waves;
+    // launches rotate over the layers, so a repeat never finds its weights in the 256 MB
+    // Infinity Cache (a decode step streams every layer once)
+    int rot = 0;
     auto launch = [&]() -> bool {
+        const int l = rot++ % ctx->c.n_layers;
         switch (which) {
-            case 0: return launch_gemv<PRO_RMSNORM, EPI_GLU>(ctx->L[0].w13_dt, w13_args(ctx, 0), ctx->stream, mb);
-            case 1: return launch_gemv<PRO_RMSNORM, EPI_QKV>(ctx->L[0].qkv_dt, qkv_args(ctx, 0), ctx->stream, mb);
-            case 2: return launch_gemv<PRO_PLAIN, EPI_RESID>(ctx->L[0].wo_dt, wo_args(ctx, 0), ctx->stream, mb);
-            case 3: return launch_gemv<PRO_PLAIN, EPI_RESID>(ctx->L[0].w2_dt, w2_args(ctx, 0), ctx->stream, mb);
+            case 0: return launch_gemv<PRO_RMSNORM, EPI_GLU>(ctx->L[l].w13_dt, w13_args(ctx, l), ctx->stream, mb);
+            case 1: return launch_gemv<PRO_RMSNORM, EPI_QKV>(ctx->L[l].qkv_dt, qkv_args(ctx, l), ctx->stream, mb);
+            case 2: return launch_gemv<PRO_PLAIN, EPI_RESID>(ctx->L[l].wo_dt, wo_args(ctx, l), ctx->stream, mb);
+            case 3: return launch_gemv<PRO_PLAIN, EPI_RESID>(ctx->L[l].w2_dt, w2_args(ctx, l), ctx->stream, mb);
             case 4: return launch_gemv<PRO_RMSNORM, EPI_STORE>(ctx->wcls_dt, cls_args(ctx), ctx->stream, mb);
             default:
-                return launch_attn(attn_args(ctx, 0), ctx->c.head_dim, ctx->qpk, ctx->c.n_kv_heads, ctx->t_max,
+                return launch_attn(attn_args(ctx, l), ctx->c.head_dim, ctx->qpk, ctx->c.n_kv_heads, ctx->t_max,
                                    ctx->stream);
         }
     };
