@@ -78,9 +78,10 @@ def test_cli_completion_matches_oracle(device_loop):
     from oracle import oracle as O
     path = fixture_path("tiny_mistral_f16.xalm")
     r = subprocess.run([CLI, path, "-n", "12", "-i", "the answer is", "-g", device_loop], capture_output=True,
-                       text=True, timeout=120)
-    assert r.returncode == 0, r.stderr
-    ids = [int(v) for v in re.search(r"tokens: \[([0-9,]*)\]", r.stdout).group(1).split(",")]
+                       timeout=120)
+    out_txt = r.stdout.decode("utf-8", errors="replace")
+    assert r.returncode == 0, r.stderr.decode(errors="replace")
+    ids = [int(v) for v in re.search(r"tokens: \[([0-9,]*)\]", out_txt).group(1).split(",")]
     xf = XalmFile(path)
     om = O.OracleModel.from_xalm(xf)
     lib = host()
@@ -101,11 +102,16 @@ def test_cli_completion_matches_oracle(device_loop):
 @pytest.mark.gpu
 def test_cli_perplexity_matches_oracle():
     from oracle import oracle as O
-    path = fixture_path("small_llama_f16.xalm")
+    # tiny_mistral: logits of O(1), so no probability underflows to 0 in sample_prob (on the
+    # small_llama fixture, |logits| ~ 87 and the reference's own perplexity is inf)
+    path = fixture_path("tiny_mistral_f16.xalm")
     text = "Q: What is the meaning of life? A: the answer is in the stars"
-    r = subprocess.run([CLI, path, "-m", "perplexity", "-i", text], capture_output=True, text=True, timeout=120)
-    assert r.returncode == 0, r.stderr
-    ppl = float(re.search(r"perplexity: ([0-9.eE+-]+)\n", r.stdout).group(1))
+    r = subprocess.run([CLI, path, "-m", "perplexity", "-i", text], capture_output=True, timeout=120)
+    out_txt = r.stdout.decode("utf-8", errors="replace")
+    assert r.returncode == 0, r.stderr.decode(errors="replace")
+    m = re.search(r"^perplexity: (\S+)$", out_txt, re.M)
+    assert m, out_txt
+    ppl = float(m.group(1))
     lib = host()
     out = (ctypes.c_int * 128)()
     n = ctypes.c_int(0)
@@ -117,4 +123,4 @@ def test_cli_perplexity_matches_oracle():
         om.forward(ids[pos], pos)
         s += np.log(O.sample_prob(om.logits(), ids[pos + 1]))
     ref = float(np.exp(-s / (len(ids) - 1)))
-    assert abs(ppl - ref) <= 1e-3 * ref
+    assert np.isfinite(ref) and abs(ppl - ref) <= 1e-3 * ref

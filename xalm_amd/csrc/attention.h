@@ -196,39 +196,44 @@ __global__ __launch_bounds__(ATTN_THREADS) void attn_split_kernel(const AttnArgs
     }
 
     // ---- partial store, then the last block of this KV head merges all splits ----
-    float* po = a.part_o + ((size_t)s * a.n_heads + g * QPK) * HD;
-    for (int idx = tid; idx < QPK * HD; idx += ATTN_THREADS)
-        po[idx] = red[idx] + red[QPK * HD + idx] + red[2 * QPK * HD + idx] + red[3 * QPK * HD + idx];
-    if (tid < 2 * QPK) a.part_ml[((size_t)s * a.n_heads + g * QPK) * 2 + tid] = ml[tid];
+    // Write-through hand-off (MI355X_MICROARCH.md, "Valid forms" table row 1): every partial
+    // is stored with an agent-scope relaxed store (sc1, bypasses the non-coherent L1), every
+    // storing wave drains vmcnt, one lane adds the ticket; the block whose add returns
+    // n_active-1 reads every partial with agent-scope relaxed (sc1) loads.  No fences.
+    uint32_t* po = (uint32_t*)(a.part_o + ((size_t)s * a.n_heads + g * QPK) * HD);
+    for (int idx = tid; idx < QPK * HD; idx += ATTN_THREADS) {
+        const float o = red[idx] + red[QPK * HD + idx] + red[2 * QPK * HD + idx] + red[3 * QPK * HD + idx];
+        __hip_atomic_store(po + idx, __builtin_bit_cast(uint32_t, o), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (tid < 2 * QPK)
+        __hip_atomic_store((uint32_t*)a.part_ml + ((size_t)s * a.n_heads + g * QPK) * 2 + tid,
+                           __builtin_bit_cast(uint32_t, ml[tid]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const int ticket = __hip_atomic_fetch_add(a.counters + g, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const int last = ticket == n_active - 1;
-        if (last) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __hip_atomic_store(a.counters + g, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+        if (last) __hip_atomic_store(a.counters + g, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         *flag = last;
     }
     __syncthreads();
     if (!*flag) return;
+    auto ld = [](const float* p) {
+        return __builtin_bit_cast(float, __hip_atomic_load((const uint32_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    };
     // merge: out = sum_s e^{m_s-M} o_s / sum_s e^{m_s-M} l_s   (per head)
     float* wts = sc;  // reuse: [QPK][n_active] weights, then [QPK] 1/den
     for (int h = wid; h < QPK; h += ATTN_THREADS / 64) {
         float M = -FLT_MAX;
         for (int j = lane; j < n_active; j += 64)
-            M = fmaxf(M, a.part_ml[((size_t)j * a.n_heads + g * QPK + h) * 2]);
+            M = fmaxf(M, ld(a.part_ml + ((size_t)j * a.n_heads + g * QPK + h) * 2));
         M = wave_max(M);
         float den = 0.f;
         for (int j = lane; j < n_active; j += 64) {
             const float* mlp = a.part_ml + ((size_t)j * a.n_heads + g * QPK + h) * 2;
-            const float f = expf(mlp[0] - M);
+            const float f = expf(ld(mlp) - M);
             wts[h * n_active + j] = f;
-            den = fmaf(f, mlp[1], den);
+            den = fmaf(f, ld(mlp + 1), den);
         }
         den = wave_sum(den);
         if (lane == 0) red[h] = den;
@@ -238,8 +243,7 @@ __global__ __launch_bounds__(ATTN_THREADS) void attn_split_kernel(const AttnArgs
         const int h = idx / HD;
         const float* w = wts + h * n_active;
         float num = 0.f;
-        for (int j = 0; j < n_active; j++)
-            num = fmaf(w[j], a.part_o[((size_t)j * a.n_heads + g * QPK) * HD + idx], num);
+        for (int j = 0; j < n_active; j++) num = fmaf(w[j], ld(a.part_o + ((size_t)j * a.n_heads + g * QPK) * HD + idx), num);
         a.out[(size_t)g * QPK * HD + idx] = num / red[h];
     }
 }

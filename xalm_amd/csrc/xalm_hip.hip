@@ -113,10 +113,11 @@ int set_err(xh_ctx* ctx, int code, const char* fmt, ...) {
 // ---------------------------------------------------------------------------------------
 // gemv launch dispatch
 // ---------------------------------------------------------------------------------------
-// Shapes (tools/gemv_bench.hip measures the alternatives): short rows (x image <= 40 KB, all
-// of Mistral's matrices but W2) use 256-thread blocks, long rows share one x image over 512.
-using ShapeShort = GemvShape<256, ROWS, UNROLL, true, 4>;
-using ShapeLong = GemvShape<512, ROWS, UNROLL, true, 4>;
+// Shapes, chosen with tools/gemv_bench.hip on MI355X (profiles/r01_gemv_bench.txt): 512-thread
+// blocks (8 waves share one x image), 2 rows x 4 chunks in flight per wave, non-temporal
+// weight loads, 16 waves per CU, no register prefetch ahead of the prologue (it spills).
+using ShapeShort = GemvShape<512, ROWS, UNROLL, true, 4, false>;
+using ShapeLong = GemvShape<512, ROWS, UNROLL, true, 4, false>;
 
 template <int DT, int PRO, int EPI, class S>
 void launch_gemv_s(const GemvArgs& a, hipStream_t s, int max_waves) {
