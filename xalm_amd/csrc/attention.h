@@ -5,14 +5,14 @@
 //   s_t = (q_h . K[t, g]) * (1/sqrtf(hd)),  t in [0, kv_len) ring slots
 //   p   = softmax(s)   (max-subtract, expf)
 //   o_h = sum_t p_t V[t, g],   g = h / (n_heads / n_kv_heads)
-// One workgroup serves one KV head and a contiguous slot range, so each K/V row is read from
-// HBM once for all q heads of its group (the CPU re-reads it per q head).  The slot range
-// length T is chosen on device from kv_len, so the grid never changes (graph replay).
-// K and V rows of the first PREF passes are requested together at kernel start: for contexts
-// up to 64 * nsplit slots the whole kernel is one HBM round trip.
-// With more than one active split, every block stores its partial (o, m, l); the last block
-// of each KV head to arrive (agent-scope release -> ticket -> acquire, cdna_hip_programming.md
-// §6 Guideline 16 / "In-launch split-K reduction") merges them: no second launch.
+// One workgroup (16 waves) serves one KV head and a contiguous slot range, so each K/V row is
+// read from HBM once for all q heads of its group (the CPU re-reads it per q head).  K and V
+// rows of ATTN_PREF passes (ATTN_PREF * 1024 / (hd/8) slots: 256 at hd = 128) are requested
+// together at kernel start, so a split of up to 256 slots is one HBM round trip.  The split
+// length T is chosen on device from kv_len (grid shape fixed for graph replay): kv_len <= 256
+// needs no merge at all.  With more than one active split, every block stores its partial
+// (o, m, l) write-through and the last block of each KV head to arrive merges them (ticket
+// protocol of MI355X_MICROARCH.md "Valid forms", row 1): no second launch, no fences.
 #pragma once
 
 #include <float.h>
@@ -21,9 +21,10 @@
 
 namespace xalm {
 
-constexpr int ATTN_THREADS = 256;
+constexpr int ATTN_THREADS = 1024;
+constexpr int ATTN_WAVES = ATTN_THREADS / 64;
 constexpr int ATTN_PREF = 4;     // K/V passes held in registers per round
-constexpr int ATTN_MIN_T = 64;   // minimum slots per split
+constexpr int ATTN_MIN_T = 256;  // minimum slots per split
 
 struct AttnArgs {
     const float* q;          // [n_heads * HD], roped
@@ -46,13 +47,21 @@ __device__ __host__ __forceinline__ int attn_split_len(const int kv_len, const i
     return t < ATTN_MIN_T ? ATTN_MIN_T : t;
 }
 
+__device__ __forceinline__ float ld_sc1(const float* p) {
+    return __builtin_bit_cast(float, __hip_atomic_load((const uint32_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ __forceinline__ void st_sc1(float* p, const float v) {
+    __hip_atomic_store((uint32_t*)p, __builtin_bit_cast(uint32_t, v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 template <int HD, int QPK>
 __global__ __launch_bounds__(ATTN_THREADS) void attn_split_kernel(const AttnArgs a) {
     constexpr int LPR = HD / 8;               // lanes per K/V row (16 B = 8 fp16 each)
     constexpr int RPP = ATTN_THREADS / LPR;   // rows per pass
+    constexpr int NO = QPK * HD;              // outputs of this block
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    float* red = (float*)smem;                               // [4][QPK][HD]
-    float* ml = red + 4 * QPK * HD;                          // [QPK][2] (+ flag)
+    float* red = (float*)smem;                               // [WAVES][NO]
+    float* ml = red + ATTN_WAVES * NO;                       // [QPK][2] (+ flag)
     float* sc = ml + ((2 * QPK + 4) & ~3);                   // [QPK][T]
     int* flag = (int*)(ml + 2 * QPK);
 
@@ -123,7 +132,7 @@ __global__ __launch_bounds__(ATTN_THREADS) void attn_split_kernel(const AttnArgs
 
     // ---- softmax statistics per head (max-subtract + expf, src/infer.cpp:280-297) ----
     const int len = t1 - t0;
-    for (int h = wid; h < QPK; h += ATTN_THREADS / 64) {
+    for (int h = wid; h < QPK; h += ATTN_WAVES) {
         float m = -FLT_MAX;
         for (int i = lane; i < len; i += 64) m = fmaxf(m, sc[h * T + i]);
         m = wave_max(m);
@@ -172,7 +181,7 @@ __global__ __launch_bounds__(ATTN_THREADS) void attn_split_kernel(const AttnArgs
             if (t < t1) pv_row(vv[p], t);
         }
     }
-    // reduce over the row slots of this wave (lanes sharing `sub`), then over waves
+    // reduce over the row slots of this wave (lanes sharing `sub`), then over waves (fixed order)
 #pragma unroll
     for (int h = 0; h < QPK; h++)
 #pragma unroll
@@ -183,31 +192,29 @@ __global__ __launch_bounds__(ATTN_THREADS) void attn_split_kernel(const AttnArgs
 #pragma unroll
         for (int h = 0; h < QPK; h++)
 #pragma unroll
-            for (int i = 0; i < 8; i++) red[(wid * QPK + h) * HD + sub * 8 + i] = acc[h][i];
+            for (int i = 0; i < 8; i++) red[wid * NO + h * HD + sub * 8 + i] = acc[h][i];
     }
     __syncthreads();
+    auto block_sum = [&](const int idx) {
+        float o = 0.f;
+#pragma unroll
+        for (int w = 0; w < ATTN_WAVES; w++) o += red[w * NO + idx];
+        return o;
+    };
     if (n_active == 1) {
-        for (int idx = tid; idx < QPK * HD; idx += ATTN_THREADS) {
-            const int h = idx / HD;
-            const float o = red[idx] + red[QPK * HD + idx] + red[2 * QPK * HD + idx] + red[3 * QPK * HD + idx];
-            a.out[(size_t)g * QPK * HD + idx] = o / ml[2 * h + 1];
-        }
+        for (int idx = tid; idx < NO; idx += ATTN_THREADS)
+            a.out[(size_t)g * NO + idx] = block_sum(idx) / ml[2 * (idx / HD) + 1];
         return;
     }
 
     // ---- partial store, then the last block of this KV head merges all splits ----
     // Write-through hand-off (MI355X_MICROARCH.md, "Valid forms" table row 1): every partial
-    // is stored with an agent-scope relaxed store (sc1, bypasses the non-coherent L1), every
-    // storing wave drains vmcnt, one lane adds the ticket; the block whose add returns
+    // is stored with an agent-scope relaxed store (sc1, not kept in the non-coherent caches),
+    // every storing wave drains vmcnt, one lane adds the ticket; the block whose add returns
     // n_active-1 reads every partial with agent-scope relaxed (sc1) loads.  No fences.
-    uint32_t* po = (uint32_t*)(a.part_o + ((size_t)s * a.n_heads + g * QPK) * HD);
-    for (int idx = tid; idx < QPK * HD; idx += ATTN_THREADS) {
-        const float o = red[idx] + red[QPK * HD + idx] + red[2 * QPK * HD + idx] + red[3 * QPK * HD + idx];
-        __hip_atomic_store(po + idx, __builtin_bit_cast(uint32_t, o), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    if (tid < 2 * QPK)
-        __hip_atomic_store((uint32_t*)a.part_ml + ((size_t)s * a.n_heads + g * QPK) * 2 + tid,
-                           __builtin_bit_cast(uint32_t, ml[tid]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    float* po = a.part_o + ((size_t)s * a.n_heads + g * QPK) * HD;
+    for (int idx = tid; idx < NO; idx += ATTN_THREADS) st_sc1(po + idx, block_sum(idx));
+    if (tid < 2 * QPK) st_sc1(a.part_ml + ((size_t)s * a.n_heads + g * QPK) * 2 + tid, ml[tid]);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) {
@@ -218,40 +225,52 @@ __global__ __launch_bounds__(ATTN_THREADS) void attn_split_kernel(const AttnArgs
     }
     __syncthreads();
     if (!*flag) return;
-    auto ld = [](const float* p) {
-        return __builtin_bit_cast(float, __hip_atomic_load((const uint32_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    };
     // merge: out = sum_s e^{m_s-M} o_s / sum_s e^{m_s-M} l_s   (per head)
-    float* wts = sc;  // reuse: [QPK][n_active] weights, then [QPK] 1/den
-    for (int h = wid; h < QPK; h += ATTN_THREADS / 64) {
-        float M = -FLT_MAX;
-        for (int j = lane; j < n_active; j += 64)
-            M = fmaxf(M, ld(a.part_ml + ((size_t)j * a.n_heads + g * QPK + h) * 2));
-        M = wave_max(M);
-        float den = 0.f;
-        for (int j = lane; j < n_active; j += 64) {
+    float* wts = sc;  // [QPK][n_active] weights (sc is free now); den in red[h]
+    for (int h = wid; h < QPK; h += ATTN_WAVES) {
+        float mv[2] = {-FLT_MAX, -FLT_MAX}, lv[2] = {0.f, 0.f};
+        int cnt = 0;
+        for (int j = lane; j < n_active; j += 64, cnt++) {  // n_active <= 128 -> at most 2 per lane
             const float* mlp = a.part_ml + ((size_t)j * a.n_heads + g * QPK + h) * 2;
-            const float f = expf(ld(mlp) - M);
+            mv[cnt & 1] = ld_sc1(mlp);
+            lv[cnt & 1] = ld_sc1(mlp + 1);
+        }
+        const float M = wave_max(fmaxf(mv[0], mv[1]));
+        float den = 0.f;
+        cnt = 0;
+        for (int j = lane; j < n_active; j += 64, cnt++) {
+            const float f = expf(mv[cnt & 1] - M);
             wts[h * n_active + j] = f;
-            den = fmaf(f, ld(mlp + 1), den);
+            den = fmaf(f, lv[cnt & 1], den);
         }
         den = wave_sum(den);
         if (lane == 0) red[h] = den;
     }
     __syncthreads();
-    for (int idx = tid; idx < QPK * HD; idx += ATTN_THREADS) {
+    for (int idx = tid; idx < NO; idx += ATTN_THREADS) {
         const int h = idx / HD;
         const float* w = wts + h * n_active;
+        const float* src = a.part_o + (size_t)g * NO + idx;
+        const size_t stride = (size_t)a.n_heads * HD;
         float num = 0.f;
-        for (int j = 0; j < n_active; j++) num = fmaf(w[j], ld(a.part_o + ((size_t)j * a.n_heads + g * QPK) * HD + idx), num);
-        a.out[(size_t)g * QPK * HD + idx] = num / red[h];
+        int j = 0;
+        for (; j + 4 <= n_active; j += 4) {
+            const float p0 = ld_sc1(src + (j + 0) * stride), p1 = ld_sc1(src + (j + 1) * stride);
+            const float p2 = ld_sc1(src + (j + 2) * stride), p3 = ld_sc1(src + (j + 3) * stride);
+            num = fmaf(w[j], p0, num);
+            num = fmaf(w[j + 1], p1, num);
+            num = fmaf(w[j + 2], p2, num);
+            num = fmaf(w[j + 3], p3, num);
+        }
+        for (; j < n_active; j++) num = fmaf(w[j], ld_sc1(src + j * stride), num);
+        a.out[(size_t)g * NO + idx] = num / red[h];
     }
 }
 
 // shared-memory bytes of attn_split_kernel<HD,QPK> for a given max split length
 inline size_t attn_smem_bytes(const int hd, const int qpk, const int t_max, const int nsplit) {
     const size_t scn = (size_t)qpk * (t_max > nsplit ? t_max : nsplit);
-    return sizeof(float) * (4 * qpk * hd + ((2 * qpk + 4) & ~3) + scn);
+    return sizeof(float) * ((size_t)ATTN_WAVES * qpk * hd + ((2 * qpk + 4) & ~3) + scn);
 }
 
 }  // namespace xalm

@@ -196,6 +196,7 @@ bool launch_attn(const AttnArgs& a, int hd, int qpk, int n_kv_heads, int t_max, 
 
 int attn_nsplit(int n_kv_heads, int max_seq_len) {
     int ns = 512 / n_kv_heads;
+    if (ns > 128) ns = 128;  // the merge holds <= 2 partials per lane
     const int cap = (max_seq_len + ATTN_MIN_T - 1) / ATTN_MIN_T;
     if (ns > cap) ns = cap;
     return ns < 1 ? 1 : ns;
@@ -410,6 +411,12 @@ int xh_create(const xh_config* cfg, int device_ordinal, xh_ctx** out) {
     if (!(c.head_dim == 16 || c.head_dim == 32 || c.head_dim == 64 || c.head_dim == 128 || c.head_dim == 256))
         return set_err(nullptr, XH_E_INVALID, "head_dim must be 16..256 power of two (got %d)", c.head_dim);
     if (c.rotary_dim > c.head_dim || c.rotary_dim < 0) return set_err(nullptr, XH_E_INVALID, "bad rotary_dim");
+    {
+        const int ns = attn_nsplit(c.n_kv_heads, c.max_seq_len);
+        if (attn_smem_bytes(c.head_dim, qpk, attn_split_len(c.max_seq_len, ns), ns) > 160 * 1024)
+            return set_err(nullptr, XH_E_INVALID, "attention tile of head_dim %d x %d q heads per kv head exceeds LDS",
+                           c.head_dim, qpk);
+    }
     if (c.act != XH_ACT_GELU && c.act != XH_ACT_SILU) return set_err(nullptr, XH_E_INVALID, "bad act");
 
     int ndev = 0;
