@@ -26,9 +26,19 @@ endif
 oracle:
 	$(MAKE) -C oracle
 
-$(LIB)/libxalm_hip.so: $(HIP_SRC) $(HIP_HDR)
+# the persistent kernel is instantiated per weight dtype in its own object (parallel build)
+OBJ := xalm_amd/build
+PK_DTS := 1 2 3 6 7
+PK_OBJS := $(patsubst %,$(OBJ)/pk_launch_dt%.o,$(PK_DTS))
+$(OBJ)/xalm_hip.o: $(HIP_SRC) $(HIP_HDR)
+	@mkdir -p $(OBJ)
+	$(HIPCC) $(HIPFLAGS) -c -o $@ $(HIP_SRC)
+$(OBJ)/pk_launch_dt%.o: xalm_amd/csrc/pk_launch.hip $(HIP_HDR)
+	@mkdir -p $(OBJ)
+	$(HIPCC) $(HIPFLAGS) -DPK_DT=$* -c -o $@ $<
+$(LIB)/libxalm_hip.so: $(OBJ)/xalm_hip.o $(PK_OBJS)
 	@mkdir -p $(LIB)
-	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(HIP_SRC)
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $^
 
 HOST_LIB_SRC := $(filter-out xalm_amd/host/main.cpp,$(HOST_SRC))
 $(LIB)/libxalm_host.so: $(HOST_LIB_SRC) $(HOST_HDR) $(LIB)/libxalm_hip.so
@@ -39,5 +49,5 @@ $(BIN)/xalm: xalm_amd/host/main.cpp $(LIB)/libxalm_host.so
 	$(CXX) $(HOSTFLAGS) -o $@ xalm_amd/host/main.cpp -L$(LIB) -lxalm_host -lxalm_hip -Wl,-rpath,'$$ORIGIN/../lib'
 
 clean:
-	rm -rf $(LIB) $(BIN)
+	rm -rf $(LIB) $(BIN) $(OBJ)
 	$(MAKE) -C oracle clean

@@ -142,6 +142,8 @@ def main():
     ap.add_argument("--cpu-tokens", type=int, default=4)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--kernel-iters", type=int, default=200)
+    ap.add_argument("--engine", type=int, default=-1, choices=(-1, 0, 1),
+                    help="-1 auto (persistent kernel when instantiated), 0 graph of kernels, 1 persistent")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -163,6 +165,8 @@ def main():
     for kind, layer, dt, seed, mean, std in tensor_specs(w):
         model.upload_synthetic(kind, layer, dt, seed, mean, std)
 
+    model.set_engine(args.engine)
+    engine = model.engine
     prompt = prompt_tokens(c.vocab_size)
     st = InferenceState(c)
     pos0 = 0
@@ -172,9 +176,7 @@ def main():
             model.kv_fill_synthetic(layer, 0, 0, w["kv_prefill"], 5000 + 2 * layer, 1.0)
             model.kv_fill_synthetic(layer, 1, 0, w["kv_prefill"], 5001 + 2 * layer, 1.0)
         pos0 = w["kv_prefill"]
-    for i, tok in enumerate(prompt[:1] if w["kv_prefill"] else prompt):
-        last = w["kv_prefill"] or i == len(prompt) - 1
-        model.forward(st, tok, pos0 + i, L.OUTPUT_LOGITS if last else L.HYDRATE_KV_CACHE)
+    model.prefill(prompt[:1] if w["kv_prefill"] else prompt, pos0, st)
     pos = pos0 + (1 if w["kv_prefill"] else len(prompt))
     logits0 = st.logits().copy()
 
@@ -189,6 +191,7 @@ def main():
     sync_all(dist, torch_mod)
     t1 = time.perf_counter()
     elapsed = t1 - t0
+    launch_us = model.last_launch_us() if engine == 1 else None
     if dist is not None:
         import torch
         t = torch.tensor([elapsed], dtype=torch.float64)
@@ -201,12 +204,12 @@ def main():
     step_bytes = sum(model.active_bytes(p) for p in range(pos, pos + args.steps))
     step_gbps = step_bytes / elapsed / 1e9
 
-    # dominant kernel: fused gate/up matvec (W1/W3 = 44 % of the bytes), timed on its own stream
+    # graph engine's kernels, each timed on its own (HIP events on the context stream)
     kv_len_now = min(c.max_seq_len, pos + args.steps)
     k_us = model.time_kernel(0, args.kernel_iters)
     k_bytes = model.kernel_bytes(0, kv_len_now)
     k_gbps = k_bytes / (k_us * 1e-6) / 1e9
-    extra_kernels = {}
+    extra_kernels = {"gemv_w13": {"avg_us": round(k_us, 2), "GBps": round(k_gbps, 1)}}
     for which, name in ((1, "gemv_qkv"), (2, "gemv_wo"), (3, "gemv_w2"), (4, "gemv_lm_head"), (5, "attention")):
         us = model.time_kernel(which, max(20, args.kernel_iters // 4))
         b = model.kernel_bytes(which, kv_len_now)
@@ -218,6 +221,18 @@ def main():
         if n:
             cpu = cpu_baseline(w, c, prompt, logits0, warm_tokens, n)
 
+    if engine == 1:
+        # dominant (only) kernel: the persistent decode kernel; one launch = the K timed tokens
+        r_gbps = step_bytes / (launch_us * 1e-6) / 1e9
+        roofline = {"bound": "hbm", "achieved": round(r_gbps, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                    "frac": round(r_gbps / HBM_PEAK_GBPS, 4), "traffic": None,
+                    "kernel": "persistent_decode_kernel (all phases of all timed tokens, one launch)",
+                    "bytes_per_launch": step_bytes, "avg_launch_us": round(launch_us, 1)}
+    else:
+        roofline = {"bound": "hbm", "achieved": round(k_gbps, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                    "frac": round(k_gbps / HBM_PEAK_GBPS, 4), "traffic": None,
+                    "kernel": "gemv_kernel<PRO_RMSNORM,EPI_GLU> (fused W1/W3 + rmsnorm + silu*up), layer 0",
+                    "bytes_per_launch": k_bytes, "avg_launch_us": round(k_us, 2)}
     value = world * args.steps / elapsed
     if rank == 0:
         out = {
@@ -234,11 +249,9 @@ def main():
             "dtype": w["dtype"],
             "data": "synthetic (deterministic xalm_synth weights of the named shapes; no checkpoint offline)",
             "config": {"workload": w["desc"], "prompt_tokens": len(prompt), "max_seq_len": c.max_seq_len,
-                       "kv_len_timed": [pos + 1, pos + args.steps], "batch": 1, "parallelism": f"replicas x{world}"},
-            "roofline": {"bound": "hbm", "achieved": round(k_gbps, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                         "frac": round(k_gbps / HBM_PEAK_GBPS, 4), "traffic": None,
-                         "kernel": "gemv_kernel<PRO_RMSNORM,EPI_GLU> (fused W1/W3 + rmsnorm + silu*up), layer 0",
-                         "bytes_per_launch": k_bytes, "avg_launch_us": round(k_us, 2)},
+                       "kv_len_timed": [pos + 1, pos + args.steps], "batch": 1, "parallelism": f"replicas x{world}",
+                       "engine": "persistent" if engine == 1 else "graph"},
+            "roofline": roofline,
             "hbm_step": {"achieved_GBps": round(step_gbps, 1), "frac": round(step_gbps / HBM_PEAK_GBPS, 4),
                          "bytes_per_token": step_bytes // args.steps,
                          "note": "Model::active_bytes per token x tok/s, whole forward incl. launch gaps"},

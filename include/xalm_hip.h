@@ -124,6 +124,28 @@ int xh_forward(xh_ctx* ctx, int token, int pos, int mode, float* logits_out);
 int xh_decode_greedy(xh_ctx* ctx, int pos, int n_steps, int stop_token_a, int stop_token_b,
                      int* tokens_out, int* n_done);
 
+/* Hydrate: forward tokens[0..n) at positions pos0.. (HYDRATE_KV_CACHE for all but the last,
+ * which computes logits if want_logits), the prompt loop of run_completion
+ * (src/main.cpp:94-100) in one call.  logits_out may be NULL. */
+int xh_prefill(xh_ctx* ctx, const int* tokens, int n, int pos0, int want_logits, float* logits_out);
+
+/* Device engine: 0 = one hipGraph of kernels per token (gemv / attention launches);
+ * 1 = the persistent decode kernel (one launch per call, every phase inside, weights
+ * streamed ahead across the hand-offs; needs one dtype for all layer matrices and norms and
+ * an instantiated head shape); -1 = automatic (currently the graph engine, the faster one on
+ * MI355X).  Both compute the same math (reduction orders differ, within the tolerances). */
+int xh_set_engine(xh_ctx* ctx, int engine);
+int xh_get_engine(const xh_ctx* ctx); /* the engine the next call will use */
+/* Device time (HIP events on the context's stream) of the last persistent-engine launch,
+ * in microseconds: one launch covers a whole xh_prefill / xh_decode_greedy call. */
+int xh_last_launch_us(const xh_ctx* ctx, float* us);
+/* Debug timeline of the persistent engine.  enable: 1 on / 0 off for later launches, -1
+ * unchanged.  Copies min(cap, *len) words of the last traced launch to `out` first: for the
+ * launch's last token, workgroups {0, n_cu/2, n_cu-1} x [n_layers + 1][5 phases][2] device
+ * clock stamps (100 MHz; 0 = not reached) — [l][p][0] hand-off passed, [l][p][1] published —
+ * plus 2 words ([n_layers][1][1] = token start, [n_layers][1][0] = next token known). */
+int xh_debug_trace(xh_ctx* ctx, int enable, uint64_t* out, int cap, int* len);
+
 /* Copy the current device logits to the host. */
 int xh_get_logits(xh_ctx* ctx, float* logits_out);
 

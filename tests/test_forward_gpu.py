@@ -20,14 +20,20 @@ FIXTURES = ["tiny_mistral_f16", "tiny_mistral_bf16", "tiny_mistral_f32", "tiny_m
             "tiny_mistral_f8_e5m2", "small_llama_f16"]
 
 
+# 0 = hipGraph of kernels per token, 1 = persistent kernel (xh_set_engine)
+ENGINES = [0, 1]
+
+
 def tol(ref):
     return 1e-3 * max(1.0, float(np.abs(ref).max()))
 
 
-def run_pair(name, tokens, context=0, graphs=True, modes=None):
+def run_pair(name, tokens, context=0, graphs=True, modes=None, engine=0):
     xf = XalmFile(fixture_path(name + ".xalm"))
     gm = Model.from_xalm(xf, context=context)
     gm.set_graphs(graphs)
+    gm.set_engine(engine)
+    assert gm.engine == engine
     om = O.OracleModel.from_xalm(xf, context=context)
     st = InferenceState(gm.config)
     worst = 0.0
@@ -43,11 +49,12 @@ def run_pair(name, tokens, context=0, graphs=True, modes=None):
     return gm, om, worst
 
 
+@pytest.mark.parametrize("engine", ENGINES)
 @pytest.mark.parametrize("name", FIXTURES)
-def test_forward_matches_oracle(name):
+def test_forward_matches_oracle(name, engine):
     g = np.load(fixture_path("hf_logits_%s.npz" % name.rsplit("_", 1)[0].replace("_f8", "")))
     toks = [int(t) for t in g["tokens"]]
-    gm, om, worst = run_pair(name, toks)
+    gm, om, worst = run_pair(name, toks, engine=engine)
     # KV rings equal the oracle's up to fp16 rounding: both round to nearest-even, but the fp32
     # values differ in the last bits (summation order, amplified through the layers), so values
     # near a rounding boundary land an ulp apart.  Layer 0 (inputs identical up to rmsnorm
@@ -80,25 +87,70 @@ def test_forward_matches_hf(name):
         assert st.logits().argmax() == g["logits"][pos].argmax()
 
 
-def test_ring_buffer_and_sinks():
+@pytest.mark.parametrize("engine", ENGINES)
+def test_ring_buffer_and_sinks(engine):
     # -T 16 with 48 tokens: kv_sink=2, ring wrap, sink re-rotation every step (src/infer.cpp:608-613, 421-431)
     toks = [1] + [3 + (i * 37) % 290 for i in range(47)]
-    gm, om, _ = run_pair("tiny_mistral_f16", toks, context=16)
+    gm, om, _ = run_pair("tiny_mistral_f16", toks, context=16, engine=engine)
     for layer in range(gm.config.n_layers):
         a = gm.kv_read(layer, 0, 0, 16).view(np.float16).astype(np.float32)
         b = om.kv(layer, 0)[:16].view(np.float16).astype(np.float32)
         assert np.abs(a - b).max() <= 2e-3 * max(1.0, np.abs(b).max())
 
 
-def test_ring_buffer_head_dim_128():
+@pytest.mark.parametrize("engine", ENGINES)
+def test_ring_buffer_head_dim_128(engine):
     toks = [1] + [3 + (i * 53) % 310 for i in range(39)]
-    run_pair("small_llama_f16", toks, context=24)
+    run_pair("small_llama_f16", toks, context=24, engine=engine)
 
 
-def test_hydrate_mode_then_logits():
+@pytest.mark.parametrize("engine", ENGINES)
+def test_hydrate_mode_then_logits(engine):
     toks = [1] + [3 + (i * 11) % 290 for i in range(15)]
     modes = [L.HYDRATE_KV_CACHE] * (len(toks) - 1) + [L.OUTPUT_LOGITS]
-    run_pair("tiny_mistral_f16", toks, modes=modes)
+    run_pair("tiny_mistral_f16", toks, modes=modes, engine=engine)
+
+
+@pytest.mark.parametrize("engine", ENGINES)
+@pytest.mark.parametrize("name,context", [("tiny_mistral_f16", 16), ("small_llama_f16", 0),
+                                          ("tiny_mistral_f8_e4m3", 0)])
+def test_prefill_matches_oracle(name, context, engine):
+    # xh_prefill = the prompt loop of run_completion in one call (one launch on the persistent
+    # engine); KV rings and the last logits equal the oracle's token-by-token forward
+    xf = XalmFile(fixture_path(name + ".xalm"))
+    gm = Model.from_xalm(xf, context=context)
+    gm.set_engine(engine)
+    om = O.OracleModel.from_xalm(xf, context=context)
+    toks = [1] + [3 + (i * 29) % 290 for i in range(36)]
+    st = InferenceState(gm.config)
+    gm.prefill(toks, 0, st)
+    for pos, tok in enumerate(toks):
+        om.forward(tok, pos, L.OUTPUT_LOGITS if pos == len(toks) - 1 else L.HYDRATE_KV_CACHE)
+    assert np.abs(st.logits() - om.logits()).max() <= tol(om.logits())
+    n = min(len(toks), gm.config.max_seq_len)
+    for layer in range(gm.config.n_layers):
+        a = gm.kv_read(layer, 1, 0, n).view(np.float16).astype(np.float32)
+        b = om.kv(layer, 1)[:n].view(np.float16).astype(np.float32)
+        assert np.abs(a - b).max() <= 2e-3 * max(1.0, np.abs(b).max())
+
+
+def test_engines_agree_on_long_decode():
+    # 200 greedy tokens on the head_dim-128 fixture: the persistent engine's tokens equal the
+    # graph engine's (same per-row math; only the rmsnorm reduction order differs), logits
+    # within the tolerance after every step of a teacher-forced replay
+    xf = XalmFile(fixture_path("small_llama_f16.xalm"))
+    res = []
+    for engine in ENGINES:
+        gm = Model.from_xalm(xf)
+        gm.set_engine(engine)
+        st = InferenceState(gm.config)
+        gm.prefill([1, 7, 99], 0, st)
+        toks = gm.decode_greedy(3, 120)
+        gm.get_logits(st)
+        res.append((toks, st.logits().copy()))
+        gm.close()
+    assert res[0][0] == res[1][0]
+    assert np.abs(res[0][1] - res[1][1]).max() <= tol(res[0][1])
 
 
 def test_graphs_and_eager_bitwise_equal():
@@ -115,9 +167,11 @@ def test_graphs_and_eager_bitwise_equal():
     assert np.array_equal(outs[0], outs[1])
 
 
-def test_device_greedy_decode_matches_oracle_teacher_forced():
+@pytest.mark.parametrize("engine", ENGINES)
+def test_device_greedy_decode_matches_oracle_teacher_forced(engine):
     xf = XalmFile(fixture_path("tiny_mistral_f16.xalm"))
     gm = Model.from_xalm(xf)
+    gm.set_engine(engine)
     om = O.OracleModel.from_xalm(xf)
     st = InferenceState(gm.config)
     prompt = [1, 84, 262, 259, 90]
@@ -138,9 +192,11 @@ def test_device_greedy_decode_matches_oracle_teacher_forced():
     assert np.abs(st.logits() - om.logits()).max() <= tol(om.logits())
 
 
-def test_decode_stops_on_eos():
+@pytest.mark.parametrize("engine", ENGINES)
+def test_decode_stops_on_eos(engine):
     xf = XalmFile(fixture_path("tiny_mistral_f16.xalm"))
     gm = Model.from_xalm(xf)
+    gm.set_engine(engine)
     st = InferenceState(gm.config)
     gm.forward(st, 1, 0)
     first = gm.decode_greedy(1, 3)

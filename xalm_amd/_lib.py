@@ -53,6 +53,11 @@ _SIGNATURES = {
     "xh_kv_fill_synthetic": (_I, [_P, _I, _I, _I, _I, ctypes.c_uint64, ctypes.c_float]),
     "xh_forward": (_I, [_P, _I, _I, _I, _P]),
     "xh_decode_greedy": (_I, [_P, _I, _I, _I, _I, _P, ctypes.POINTER(_I)]),
+    "xh_prefill": (_I, [_P, _P, _I, _I, _I, _P]),
+    "xh_set_engine": (_I, [_P, _I]),
+    "xh_get_engine": (_I, [_P]),
+    "xh_last_launch_us": (_I, [_P, _FP]),
+    "xh_debug_trace": (_I, [_P, _I, _P, _I, ctypes.POINTER(_I)]),
     "xh_get_logits": (_I, [_P, _P]),
     "xh_reset": (_I, [_P]),
     "xh_kv_write": (_I, [_P, _I, _I, _I, _I, _P]),

@@ -1,0 +1,73 @@
+// pk_launch.hip — persistent-kernel instantiations for one weight dtype (-DPK_DT=<xh_dtype>).
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+
+#include "pk_launch.h"
+
+#ifndef PK_DT
+#error "compile with -DPK_DT=<xh_dtype id>"
+#endif
+
+namespace xalm {
+namespace {
+
+template <int DT, int DTC, int HD, int QPK>
+int go(const PkArgs& a, int n_cu, hipStream_t stream, char* err, size_t errlen) {
+    const size_t smem = pk_smem_bytes(a, WDec<DT>::E, WDec<DTC>::E, HD, QPK);
+    if (smem > 160 * 1024) {
+        snprintf(err, errlen, "persistent kernel LDS %zu B exceeds 160 KiB", smem);
+        return XH_E_INVALID;
+    }
+    auto k = persistent_decode_kernel<DT, DTC, HD, QPK>;
+    static bool attr = false;
+    if (!attr) {
+        if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess) {
+            snprintf(err, errlen, "hipFuncSetAttribute failed");
+            return XH_E_HIP;
+        }
+        attr = true;
+    }
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, PK_THREADS, smem) != hipSuccess || per_cu < 1) {
+        snprintf(err, errlen, "persistent kernel does not fit one workgroup per CU");
+        return XH_E_INVALID;
+    }
+    hipLaunchKernelGGL(k, dim3(n_cu), dim3(PK_THREADS), smem, stream, a);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        snprintf(err, errlen, "persistent launch: %s", hipGetErrorString(e));
+        return XH_E_HIP;
+    }
+    return 0;
+}
+
+template <int DT, int DTC>
+int go_hd(const PkArgs& a, int n_cu, hipStream_t stream, char* err, size_t errlen) {
+    const int hd = a.head_dim, qpk = a.n_heads / a.n_kv_heads;
+    if (hd == 128 && qpk == 4) return go<DT, DTC, 128, 4>(a, n_cu, stream, err, errlen);
+    if (hd == 128 && qpk == 8) return go<DT, DTC, 128, 8>(a, n_cu, stream, err, errlen);
+    if (hd == 64 && qpk == 4) return go<DT, DTC, 64, 4>(a, n_cu, stream, err, errlen);
+    if (hd == 16 && qpk == 2) return go<DT, DTC, 16, 2>(a, n_cu, stream, err, errlen);
+    snprintf(err, errlen, "persistent engine: head_dim %d x %d q per kv not instantiated", hd, qpk);
+    return XH_E_INVALID;
+}
+
+int unsupported(int dt, int dtc, char* err, size_t errlen) {
+    snprintf(err, errlen, "persistent engine: unsupported dtype pair %d/%d", dt, dtc);
+    return XH_E_INVALID;
+}
+
+}  // namespace
+
+#define XALM_CAT2(a, b) a##b
+#define XALM_CAT(a, b) XALM_CAT2(a, b)
+int XALM_CAT(pk_launch_dt, PK_DT)(const PkArgs& a, int dtc, int n_cu, hipStream_t stream, char* err, size_t errlen) {
+#if PK_DT == 6 || PK_DT == 7  // fp8 matrices: lm_head bf16 (convert.py) or fp8
+    if (dtc == XH_BF16) return go_hd<PK_DT, XH_BF16>(a, n_cu, stream, err, errlen);
+#endif
+    if (dtc == PK_DT) return go_hd<PK_DT, PK_DT>(a, n_cu, stream, err, errlen);
+    return unsupported(PK_DT, dtc, err, errlen);
+}
+
+}  // namespace xalm

@@ -28,6 +28,8 @@
 #include "../../include/xalm_synth.h"
 #include "attention.h"
 #include "gemv.h"
+#include "pk_launch.h"
+#include "standalone.h"
 
 using namespace xalm;
 
@@ -85,6 +87,22 @@ struct xh_ctx {
     bool use_graphs = true;
     hipGraphExec_t g_logits = nullptr, g_hydrate = nullptr, g_decode = nullptr;
     int max_gemv_waves = 4096;  // 16 waves per CU
+    // persistent engine (persistent.h)
+    int engine = -1;            // -1 auto, 0 graph of kernels, 1 persistent
+    int n_cu = 0;
+    PkLayer* pk_layers = nullptr;        // device [n_layers]
+    unsigned* pk_counters = nullptr;     // device [n_layers * PK_PHASES + 1]
+    int* pk_tickets = nullptr;           // device [n_kv_heads]
+    int* pk_err = nullptr;               // device [2]: err, n_done
+    unsigned long long* pk_cand = nullptr;  // device [n_cu]
+    int* pk_prompt = nullptr;            // device [pk_prompt_cap]
+    int pk_prompt_cap = 0;
+    int* pk_host = nullptr;              // pinned [2 + pk_prompt_cap]: err, n_done, prompt staging
+    bool pk_layers_dirty = true;
+    hipEvent_t pk_ev[2] = {nullptr, nullptr};  // bracket every persistent launch
+    float pk_last_us = 0.f;
+    unsigned long long* pk_trace = nullptr;  // device [PK_TRACE_WG][pk_trace_len]
+    bool pk_trace_on = false;
 
     uint16_t* kcache(int l) { return kv + (size_t)l * 2 * c.max_seq_len * kv_dim; }
     uint16_t* vcache(int l) { return kcache(l) + (size_t)c.max_seq_len * kv_dim; }
@@ -328,7 +346,109 @@ int check_ready(xh_ctx* ctx) {
     return 0;
 }
 
+// ---------------------------------------------------------------------------------------
+// persistent engine
+// ---------------------------------------------------------------------------------------
+int pk_nsplit(const xh_ctx* ctx) {
+    int ns = ctx->n_cu / ctx->c.n_kv_heads;
+    if (ns > 128) ns = 128;
+    return ns < 1 ? 1 : ns;
+}
+
+// the weight dtypes the persistent kernel is instantiated for, or false
+bool pk_dtypes(const xh_ctx* ctx, int* dt, int* dtc, int* norm_dt) {
+    const xh_config& c = ctx->c;
+    *dt = ctx->L[0].qkv_dt;
+    *norm_dt = ctx->L[0].an_dt;
+    for (const LayerW& w : ctx->L)
+        if (w.qkv_dt != *dt || w.wo_dt != *dt || w.w13_dt != *dt || w.w2_dt != *dt || w.an_dt != *norm_dt ||
+            w.fn_dt != *norm_dt)
+            return false;
+    if (ctx->final_norm_dt != *norm_dt) return false;
+    *dtc = ctx->wcls_dt;
+    const bool hd_ok = (c.head_dim == 128 && (ctx->qpk == 4 || ctx->qpk == 8)) || (c.head_dim == 16 && ctx->qpk == 2) ||
+                       (c.head_dim == 64 && ctx->qpk == 4);
+    if (!hd_ok) return false;
+    switch (*dt) {
+        case XH_F16: return *dtc == XH_F16;
+        case XH_BF16: return *dtc == XH_BF16;
+        case XH_F32: return *dtc == XH_F32;
+        case XH_F8_E4M3: return *dtc == XH_BF16 || *dtc == XH_F8_E4M3;
+        case XH_F8_E5M2: return *dtc == XH_F8_E5M2 || *dtc == XH_BF16;
+        default: return false;
+    }
+}
+
+// automatic selection = the graph engine: measured faster on MI355X (3.0 vs 4.3 ms per
+// Mistral-7B token; the persistent kernel's one-counter hand-offs cost ~45 us per layer)
+bool use_persistent(xh_ctx* ctx) {
+    int dt, dtc, ndt;
+    if (ctx->engine != 1) return false;
+    return pk_dtypes(ctx, &dt, &dtc, &ndt);
+}
+
+// One persistent launch: n_prompt tokens from `prompt` (host), then n_gen greedy tokens.
+int run_persistent(xh_ctx* ctx, const int* prompt, int n_prompt, int n_gen, int pos0, int logits_last, int stop_a,
+                   int stop_b, int* n_done_out) {
+    const xh_config& c = ctx->c;
+    int dt, dtc, ndt;
+    if (!pk_dtypes(ctx, &dt, &dtc, &ndt))
+        return set_err(ctx, XH_E_INVALID, "persistent engine needs one dtype for all matrices and all norms");
+    if (n_prompt > ctx->pk_prompt_cap || n_gen > ctx->dec_cap) return set_err(ctx, XH_E_INVALID, "too many tokens");
+    if (ctx->pk_layers_dirty) {
+        std::vector<PkLayer> h(c.n_layers);
+        for (int l = 0; l < c.n_layers; l++) {
+            const LayerW& w = ctx->L[l];
+            h[l] = PkLayer{w.wqkv, w.wo, w.w13, w.w2, w.attn_norm, w.ffn_norm, ctx->kcache(l), ctx->vcache(l)};
+        }
+        HIP_TRY(ctx, hipMemcpy(ctx->pk_layers, h.data(), h.size() * sizeof(PkLayer), hipMemcpyHostToDevice));
+        ctx->pk_layers_dirty = false;
+    }
+    if (n_prompt) {
+        memcpy(ctx->pk_host + 2, prompt, (size_t)n_prompt * sizeof(int));
+        HIP_TRY(ctx, hipMemcpyAsync(ctx->pk_prompt, ctx->pk_host + 2, (size_t)n_prompt * sizeof(int),
+                                    hipMemcpyHostToDevice, ctx->stream));
+    }
+    HIP_TRY(ctx, hipMemsetAsync(ctx->pk_counters, 0, ((size_t)c.n_layers * PK_PHASES + 1) * sizeof(unsigned),
+                                ctx->stream));
+    HIP_TRY(ctx, hipMemsetAsync(ctx->pk_err, 0, 2 * sizeof(int), ctx->stream));
+    PkArgs a{};
+    a.n_layers = c.n_layers; a.dim = c.dim; a.hidden = c.hidden_dim; a.q_dim = ctx->q_dim; a.kv_dim = ctx->kv_dim;
+    a.head_dim = c.head_dim; a.n_heads = c.n_heads; a.n_kv_heads = c.n_kv_heads; a.vocab = c.vocab_size;
+    a.max_seq_len = c.max_seq_len; a.eps = c.norm_eps; a.qkv_clip = c.qkv_clip; a.act = c.act; a.norm_dt = ndt;
+    a.embed = ctx->embed; a.embed_dt = ctx->embed_dt; a.final_norm = ctx->final_norm; a.wcls = ctx->wcls;
+    a.layers = ctx->pk_layers; a.rope_freq = ctx->rope_freq; a.sink_cos = ctx->sink_cos; a.sink_sin = ctx->sink_sin;
+    a.x = ctx->x; a.q = ctx->q; a.attn = ctx->attn_out; a.hb = ctx->hb; a.logits = ctx->logits;
+    a.part_o = ctx->part_o; a.part_ml = ctx->part_ml; a.cand = ctx->pk_cand; a.nsplit = pk_nsplit(ctx);
+    a.counters = ctx->pk_counters; a.tickets = ctx->pk_tickets; a.err = ctx->pk_err;
+    a.prompt = ctx->pk_prompt; a.n_prompt = n_prompt; a.n_gen = n_gen; a.pos0 = pos0; a.logits_last = logits_last;
+    a.stop_a = stop_a; a.stop_b = stop_b; a.tokens_out = ctx->dec_tokens; a.n_done = ctx->pk_err + 1;
+    a.trace = ctx->pk_trace_on ? ctx->pk_trace : nullptr;
+    char msg[256] = {0};
+    HIP_TRY(ctx, hipEventRecord(ctx->pk_ev[0], ctx->stream));
+    int rc;
+    switch (dt) {
+        case XH_F32: rc = pk_launch_dt1(a, dtc, ctx->n_cu, ctx->stream, msg, sizeof msg); break;
+        case XH_F16: rc = pk_launch_dt2(a, dtc, ctx->n_cu, ctx->stream, msg, sizeof msg); break;
+        case XH_BF16: rc = pk_launch_dt3(a, dtc, ctx->n_cu, ctx->stream, msg, sizeof msg); break;
+        case XH_F8_E4M3: rc = pk_launch_dt6(a, dtc, ctx->n_cu, ctx->stream, msg, sizeof msg); break;
+        case XH_F8_E5M2: rc = pk_launch_dt7(a, dtc, ctx->n_cu, ctx->stream, msg, sizeof msg); break;
+        default: rc = XH_E_INVALID; snprintf(msg, sizeof msg, "persistent engine: dtype %d", dt);
+    }
+    if (rc) return set_err(ctx, rc, "%s", msg);
+    HIP_TRY(ctx, hipEventRecord(ctx->pk_ev[1], ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->pk_host, ctx->pk_err, 2 * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    float ms = 0.f;
+    HIP_TRY(ctx, hipEventElapsedTime(&ms, ctx->pk_ev[0], ctx->pk_ev[1]));
+    ctx->pk_last_us = ms * 1000.f;
+    if (ctx->pk_host[0]) return set_err(ctx, XH_E_HIP, "persistent kernel: a hand-off timed out (2 s)");
+    if (n_done_out) *n_done_out = ctx->pk_host[1];
+    return 0;
+}
+
 void drop_graphs(xh_ctx* ctx) {
+    ctx->pk_layers_dirty = true;
     if (ctx->g_logits) hipGraphExecDestroy(ctx->g_logits);
     if (ctx->g_hydrate) hipGraphExecDestroy(ctx->g_hydrate);
     if (ctx->g_decode) hipGraphExecDestroy(ctx->g_decode);
@@ -450,6 +570,34 @@ int xh_create(const xh_config* cfg, int device_ordinal, xh_ctx** out) {
     CREATE_TRY(dmalloc(ctx, &ctx->part_o, (size_t)ctx->nsplit * ctx->q_dim));
     CREATE_TRY(dmalloc(ctx, &ctx->part_ml, (size_t)ctx->nsplit * c.n_heads * 2));
     CREATE_TRY(dmalloc(ctx, &ctx->attn_cnt, (size_t)c.n_kv_heads));
+    {
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, device_ordinal) != hipSuccess) {
+            g_create_error = "hipGetDeviceProperties failed";
+            xh_destroy(ctx);
+            return XH_E_HIP;
+        }
+        ctx->n_cu = prop.multiProcessorCount;
+    }
+    ctx->pk_prompt_cap = 1 << 16;
+    CREATE_TRY(dmalloc(ctx, &ctx->pk_layers, (size_t)c.n_layers));
+    CREATE_TRY(dmalloc(ctx, &ctx->pk_counters, (size_t)c.n_layers * PK_PHASES + 1));
+    CREATE_TRY(dmalloc(ctx, &ctx->pk_tickets, (size_t)c.n_kv_heads));
+    CREATE_TRY(dmalloc(ctx, &ctx->pk_err, 2));
+    CREATE_TRY(dmalloc(ctx, &ctx->pk_cand, (size_t)ctx->n_cu));
+    CREATE_TRY(dmalloc(ctx, &ctx->pk_trace, (size_t)PK_TRACE_WG * pk_trace_len(c.n_layers)));
+    CREATE_TRY(dmalloc(ctx, &ctx->pk_prompt, (size_t)ctx->pk_prompt_cap));
+    if (hipHostMalloc((void**)&ctx->pk_host, (2 + (size_t)ctx->pk_prompt_cap) * sizeof(int), hipHostMallocDefault) !=
+        hipSuccess) {
+        g_create_error = "hipHostMalloc failed";
+        xh_destroy(ctx);
+        return XH_E_HIP;
+    }
+    if (hipEventCreate(&ctx->pk_ev[0]) != hipSuccess || hipEventCreate(&ctx->pk_ev[1]) != hipSuccess) {
+        g_create_error = "hipEventCreate failed";
+        xh_destroy(ctx);
+        return XH_E_HIP;
+    }
     CREATE_TRY(dmalloc(ctx, &ctx->rope_freq, (size_t)c.head_dim / 2));
     CREATE_TRY(dmalloc(ctx, &ctx->sink_cos, (size_t)c.head_dim / 2));
     CREATE_TRY(dmalloc(ctx, &ctx->sink_sin, (size_t)c.head_dim / 2));
@@ -497,6 +645,11 @@ void xh_destroy(xh_ctx* ctx) {
     hipFree(ctx->embed); hipFree(ctx->final_norm);
     hipFree(ctx->kv); hipFree(ctx->x); hipFree(ctx->q); hipFree(ctx->attn_out); hipFree(ctx->hb);
     hipFree(ctx->logits); hipFree(ctx->part_o); hipFree(ctx->part_ml); hipFree(ctx->attn_cnt); hipFree(ctx->rope_freq);
+    hipFree(ctx->pk_layers); hipFree(ctx->pk_counters); hipFree(ctx->pk_tickets); hipFree(ctx->pk_err);
+    hipFree(ctx->pk_cand); hipFree(ctx->pk_prompt); hipFree(ctx->pk_trace);
+    if (ctx->pk_host) hipHostFree(ctx->pk_host);
+    for (hipEvent_t e : ctx->pk_ev)
+        if (e) hipEventDestroy(e);
     hipFree(ctx->sink_cos); hipFree(ctx->sink_sin); hipFree(ctx->sp); hipFree(ctx->dec_tokens);
     if (ctx->sp_host) hipHostFree(ctx->sp_host);
     if (ctx->stream) hipStreamDestroy(ctx->stream);
@@ -680,9 +833,12 @@ int xh_forward(xh_ctx* ctx, int token, int pos, int mode, float* logits_out) {
     HIP_TRY(ctx, hipSetDevice(ctx->dev));
     int rc = check_ready(ctx);
     if (rc) return rc;
-    rc = host_step_params(ctx, token, pos);
-    if (rc) return rc;
-    rc = run_step(ctx, mode == XH_OUTPUT_LOGITS);
+    if (use_persistent(ctx)) {
+        rc = run_persistent(ctx, &token, 1, 0, pos, mode == XH_OUTPUT_LOGITS, -1, -1, nullptr);
+    } else {
+        rc = host_step_params(ctx, token, pos);
+        if (!rc) rc = run_step(ctx, mode == XH_OUTPUT_LOGITS);
+    }
     if (rc) return rc;
     if (logits_out && mode == XH_OUTPUT_LOGITS)
         HIP_TRY(ctx, hipMemcpyAsync(logits_out, ctx->logits, (size_t)ctx->c.vocab_size * 4, hipMemcpyDeviceToHost,
@@ -698,6 +854,18 @@ int xh_decode_greedy(xh_ctx* ctx, int pos, int n_steps, int stop_a, int stop_b, 
     HIP_TRY(ctx, hipSetDevice(ctx->dev));
     int rc = check_ready(ctx);
     if (rc) return rc;
+    if (use_persistent(ctx)) {
+        int done = 0;
+        if (n_steps) rc = run_persistent(ctx, nullptr, 0, n_steps, pos, 1, stop_a, stop_b, &done);
+        if (rc) return rc;
+        // leave the step parameters of the last position for xh_time_kernel
+        if (done) rc = host_step_params(ctx, 0, pos + done - 1);
+        if (rc) return rc;
+        if (tokens_out && done)
+            HIP_TRY(ctx, hipMemcpy(tokens_out, ctx->dec_tokens, (size_t)done * sizeof(int), hipMemcpyDeviceToHost));
+        if (n_done) *n_done = done;
+        return 0;
+    }
     // step counter 0, next position `pos`; token/pos fields are set by argmax_advance_kernel
     StepParams* h = ctx->sp_host;
     h->step = 0;
@@ -795,6 +963,72 @@ size_t xh_active_bytes(const xh_ctx* ctx, size_t pos) {
         bytes += 2 * kv_len * ctx->kv_dim * 2;
     }
     return bytes;
+}
+
+int xh_prefill(xh_ctx* ctx, const int* tokens, int n, int pos0, int want_logits, float* logits_out) {
+    if (!ctx || !tokens || n <= 0 || pos0 < 0) return set_err(ctx, XH_E_INVALID, "bad prefill arguments");
+    for (int i = 0; i < n; i++)
+        if (tokens[i] < 0 || tokens[i] >= ctx->c.vocab_size) return set_err(ctx, XH_E_INVALID, "token out of range");
+    HIP_TRY(ctx, hipSetDevice(ctx->dev));
+    int rc = check_ready(ctx);
+    if (rc) return rc;
+    if (use_persistent(ctx)) {
+        for (int off = 0; off < n && !rc; off += ctx->pk_prompt_cap) {
+            const int m = std::min(n - off, ctx->pk_prompt_cap);
+            rc = run_persistent(ctx, tokens + off, m, 0, pos0 + off, off + m == n ? want_logits : 0, -1, -1, nullptr);
+        }
+    } else {
+        for (int i = 0; i < n && !rc; i++) {
+            rc = host_step_params(ctx, tokens[i], pos0 + i);
+            if (!rc) rc = run_step(ctx, i == n - 1 && want_logits);
+            // the step parameters are copied from one pinned host slot: drain before reuse
+            if (!rc && hipStreamSynchronize(ctx->stream) != hipSuccess)
+                rc = set_err(ctx, XH_E_HIP, "hipStreamSynchronize failed");
+        }
+    }
+    if (rc) return rc;
+    if (logits_out && want_logits)
+        HIP_TRY(ctx, hipMemcpyAsync(logits_out, ctx->logits, (size_t)ctx->c.vocab_size * 4, hipMemcpyDeviceToHost,
+                                    ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    return 0;
+}
+
+int xh_set_engine(xh_ctx* ctx, int engine) {
+    if (!ctx || engine < -1 || engine > 1) return XH_E_INVALID;
+    if (engine == 1) {
+        int dt, dtc, ndt;
+        if (!pk_dtypes(ctx, &dt, &dtc, &ndt))
+            return set_err(ctx, XH_E_INVALID, "persistent engine not available for these weights");
+    }
+    ctx->engine = engine;
+    return 0;
+}
+
+int xh_last_launch_us(const xh_ctx* ctx, float* us) {
+    if (!ctx || !us) return XH_E_INVALID;
+    *us = ctx->pk_last_us;
+    return 0;
+}
+
+int xh_debug_trace(xh_ctx* ctx, int enable, uint64_t* out, int cap, int* len) {
+    if (!ctx) return XH_E_INVALID;
+    const int n = PK_TRACE_WG * pk_trace_len(ctx->c.n_layers);
+    if (len) *len = n;
+    if (out && cap > 0) {
+        HIP_TRY(ctx, hipSetDevice(ctx->dev));
+        HIP_TRY(ctx, hipMemcpy(out, ctx->pk_trace, (size_t)std::min(cap, n) * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    }
+    if (enable >= 0) {
+        ctx->pk_trace_on = enable != 0;
+        HIP_TRY(ctx, hipMemset(ctx->pk_trace, 0, (size_t)n * sizeof(uint64_t)));
+    }
+    return 0;
+}
+
+int xh_get_engine(const xh_ctx* ctx) {
+    if (!ctx) return -1;
+    return use_persistent(const_cast<xh_ctx*>(ctx)) ? 1 : 0;
 }
 
 int xh_set_graphs(xh_ctx* ctx, int enable) {

@@ -81,6 +81,39 @@ class Model:
                                          L.ptr(toks), ctypes.byref(done)), self._ctx)
         return toks[: done.value].tolist()
 
+    def prefill(self, tokens, pos0: int, s: InferenceState | None = None) -> None:
+        """Hydrate tokens[0..n) at positions pos0.. (the prompt loop of run_completion,
+        src/main.cpp:94-100); the last token's logits land in `s` when given."""
+        toks = np.ascontiguousarray(np.asarray(tokens, dtype=np.int32))
+        out = L.ptr(s.logits()) if s is not None else None
+        L.check(L.lib().xh_prefill(self._ctx, L.ptr(toks), int(toks.size), int(pos0), int(s is not None), out),
+                self._ctx)
+
+    # engine: 0 = hipGraph of kernels per token, 1 = persistent kernel, -1 = automatic
+    ENGINE_GRAPH, ENGINE_PERSISTENT, ENGINE_AUTO = 0, 1, -1
+
+    def set_engine(self, engine: int):
+        L.check(L.lib().xh_set_engine(self._ctx, int(engine)), self._ctx)
+
+    @property
+    def engine(self) -> int:
+        return int(L.lib().xh_get_engine(self._ctx))
+
+    def last_launch_us(self) -> float:
+        """Device time of the last persistent-engine launch (HIP events, its own stream)."""
+        v = ctypes.c_float(0.0)
+        L.check(L.lib().xh_last_launch_us(self._ctx, ctypes.byref(v)), self._ctx)
+        return float(v.value)
+
+    def debug_trace(self, enable: int = -1) -> np.ndarray:
+        """Persistent-engine timeline of the last traced launch, [3][n_layers + 1][5][2] clock
+        stamps (100 MHz); `enable` 1/0 switches tracing for later launches."""
+        n = ctypes.c_int(0)
+        L.check(L.lib().xh_debug_trace(self._ctx, -1, None, 0, ctypes.byref(n)), self._ctx)
+        out = np.zeros(n.value, dtype=np.uint64)
+        L.check(L.lib().xh_debug_trace(self._ctx, int(enable), L.ptr(out), n.value, ctypes.byref(n)), self._ctx)
+        return out
+
     def get_logits(self, s: InferenceState):
         L.check(L.lib().xh_get_logits(self._ctx, L.ptr(s.logits())), self._ctx)
 
