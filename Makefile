@@ -26,14 +26,15 @@ endif
 oracle:
 	$(MAKE) -C oracle
 
-# the persistent kernel is instantiated per weight dtype in its own object (parallel build)
+# the persistent and fused attention + Wo kernels are instantiated per weight dtype in their own
+# objects (parallel build)
 OBJ := xalm_amd/build
-PK_DTS := 1 2 3 6 7
-PK_OBJS := $(patsubst %,$(OBJ)/pk_launch_dt%.o,$(PK_DTS))
+PK_DTS := 1 2 3 6 7 9
+PK_OBJS := $(patsubst %,$(OBJ)/dt_launch_dt%.o,$(PK_DTS))
 $(OBJ)/xalm_hip.o: $(HIP_SRC) $(HIP_HDR)
 	@mkdir -p $(OBJ)
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $(HIP_SRC)
-$(OBJ)/pk_launch_dt%.o: xalm_amd/csrc/pk_launch.hip $(HIP_HDR)
+$(OBJ)/dt_launch_dt%.o: xalm_amd/csrc/dt_launch.hip $(HIP_HDR)
 	@mkdir -p $(OBJ)
 	$(HIPCC) $(HIPFLAGS) -DPK_DT=$* -c -o $@ $<
 $(LIB)/libxalm_hip.so: $(OBJ)/xalm_hip.o $(PK_OBJS)

@@ -20,20 +20,27 @@ FIXTURES = ["tiny_mistral_f16", "tiny_mistral_bf16", "tiny_mistral_f32", "tiny_m
             "tiny_mistral_f8_e5m2", "small_llama_f16"]
 
 
-# 0 = hipGraph of kernels per token, 1 = persistent kernel (xh_set_engine)
-ENGINES = [0, 1]
+# "graph": hipGraph of kernels per token (attention + Wo fused in one launch, the default);
+# "graph_split": the same with attention and Wo as two launches; "persistent": one persistent
+# kernel per call (xh_set_engine(1))
+ENGINES = ["graph", "graph_split", "persistent"]
+
+
+def configure(gm, engine):
+    gm.set_engine(1 if engine == "persistent" else 0)
+    gm.set_option(L.OPT_FUSE_ATTN_WO, 0 if engine == "graph_split" else 1)
+    assert gm.engine == (1 if engine == "persistent" else 0)
 
 
 def tol(ref):
     return 1e-3 * max(1.0, float(np.abs(ref).max()))
 
 
-def run_pair(name, tokens, context=0, graphs=True, modes=None, engine=0):
+def run_pair(name, tokens, context=0, graphs=True, modes=None, engine="graph"):
     xf = XalmFile(fixture_path(name + ".xalm"))
     gm = Model.from_xalm(xf, context=context)
     gm.set_graphs(graphs)
-    gm.set_engine(engine)
-    assert gm.engine == engine
+    configure(gm, engine)
     om = O.OracleModel.from_xalm(xf, context=context)
     st = InferenceState(gm.config)
     worst = 0.0
@@ -59,7 +66,7 @@ def test_forward_matches_oracle(name, engine):
     # values differ in the last bits (summation order, amplified through the layers), so values
     # near a rounding boundary land an ulp apart.  Layer 0 (inputs identical up to rmsnorm
     # order): <= 1 fp16 ulp of the element; every layer: <= 1e-3 of the ring's max |value|;
-    # most elements bit-identical.
+    # most elements bit-identical (DPP reduction order: up to ~10 % flip in the tiny model).
     c = gm.config
     n = len(toks)
     for layer in range(c.n_layers):
@@ -67,7 +74,7 @@ def test_forward_matches_oracle(name, engine):
             a = gm.kv_read(layer, which, 0, n).view(np.float16).astype(np.float32)
             b = om.kv(layer, which)[:n].view(np.float16).astype(np.float32)
             d = np.abs(a - b)
-            assert (d > 0).mean() < 0.1, (layer, which, (d > 0).mean())
+            assert (d > 0).mean() < 0.25, (layer, which, (d > 0).mean())
             assert d.max() <= 1e-3 * np.abs(b).max(), (layer, which, float(d.max()))
             if layer == 0:
                 assert np.all(d <= np.abs(b) * 2.0 ** -10 + 2.0 ** -24), (which, float(d.max()))
@@ -119,7 +126,7 @@ def test_prefill_matches_oracle(name, context, engine):
     # engine); KV rings and the last logits equal the oracle's token-by-token forward
     xf = XalmFile(fixture_path(name + ".xalm"))
     gm = Model.from_xalm(xf, context=context)
-    gm.set_engine(engine)
+    configure(gm, engine)
     om = O.OracleModel.from_xalm(xf, context=context)
     toks = [1] + [3 + (i * 29) % 290 for i in range(36)]
     st = InferenceState(gm.config)
@@ -142,15 +149,16 @@ def test_engines_agree_on_long_decode():
     res = []
     for engine in ENGINES:
         gm = Model.from_xalm(xf)
-        gm.set_engine(engine)
+        configure(gm, engine)
         st = InferenceState(gm.config)
         gm.prefill([1, 7, 99], 0, st)
         toks = gm.decode_greedy(3, 120)
         gm.get_logits(st)
         res.append((toks, st.logits().copy()))
         gm.close()
-    assert res[0][0] == res[1][0]
-    assert np.abs(res[0][1] - res[1][1]).max() <= tol(res[0][1])
+    for toks, lg in res[1:]:
+        assert toks == res[0][0]
+        assert np.abs(lg - res[0][1]).max() <= tol(res[0][1])
 
 
 def test_graphs_and_eager_bitwise_equal():
@@ -171,7 +179,7 @@ def test_graphs_and_eager_bitwise_equal():
 def test_device_greedy_decode_matches_oracle_teacher_forced(engine):
     xf = XalmFile(fixture_path("tiny_mistral_f16.xalm"))
     gm = Model.from_xalm(xf)
-    gm.set_engine(engine)
+    configure(gm, engine)
     om = O.OracleModel.from_xalm(xf)
     st = InferenceState(gm.config)
     prompt = [1, 84, 262, 259, 90]
@@ -196,7 +204,7 @@ def test_device_greedy_decode_matches_oracle_teacher_forced(engine):
 def test_decode_stops_on_eos(engine):
     xf = XalmFile(fixture_path("tiny_mistral_f16.xalm"))
     gm = Model.from_xalm(xf)
-    gm.set_engine(engine)
+    configure(gm, engine)
     st = InferenceState(gm.config)
     gm.forward(st, 1, 0)
     first = gm.decode_greedy(1, 3)
@@ -218,3 +226,25 @@ def test_upload_validation():
     st = InferenceState(gm.config)
     with pytest.raises(L.XhError):
         gm.forward(st, 1, 0)  # weights missing
+
+
+@pytest.mark.parametrize("engine", ENGINES)
+def test_multi_split_attention_in_model(engine):
+    # -T 1024 on the head_dim-128 fixture: kv_len 300 runs attention in several splits whose
+    # partials are merged in-launch (ticket), inside the fused attention + Wo launch too
+    xf = XalmFile(fixture_path("small_llama_f16.xalm"))
+    gm = Model.from_xalm(xf, context=1024)
+    configure(gm, engine)
+    om = O.OracleModel.from_xalm(xf, context=1024)
+    toks = [1] + [3 + (i * 71) % 310 for i in range(299)]
+    st = InferenceState(gm.config)
+    gm.prefill(toks, 0, st)
+    for pos, tok in enumerate(toks):
+        om.forward(tok, pos, L.OUTPUT_LOGITS if pos == len(toks) - 1 else L.HYDRATE_KV_CACHE)
+    assert np.abs(st.logits() - om.logits()).max() <= tol(om.logits())
+    nxt = gm.decode_greedy(len(toks), 4)
+    assert len(nxt) == 4
+    gm.get_logits(st)
+    for i, t in enumerate(nxt):
+        om.forward(t, len(toks) + i)
+    assert np.abs(st.logits() - om.logits()).max() <= tol(om.logits())

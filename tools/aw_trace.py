@@ -1,0 +1,61 @@
+"""Timeline of one fused attention + Wo launch (the last layer of the last decoded token)."""
+import argparse
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402
+from xalm_amd.model import InferenceState, Model  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--workload", default="mistral-7b-f16")
+    args = ap.parse_args()
+    w = bench.WORKLOADS[args.workload]
+    c = bench.make_config(w)
+    m = Model(c)
+    for kind, layer, dt, seed, mean, std in bench.tensor_specs(w):
+        m.upload_synthetic(kind, layer, dt, seed, mean, std)
+    st = InferenceState(c)
+    prompt = bench.prompt_tokens(c.vocab_size)
+    m.prefill(prompt, 0, st)
+    m.decode_greedy(len(prompt), 200)
+    m.debug_trace(2)
+    m.decode_greedy(len(prompt) + 200, 2)
+    tr = m.debug_trace(0).astype(np.int64)
+    nkv = c.n_kv_heads
+    n = tr.size // 8
+    t = tr[: n * 8].reshape(n, 8)
+    used = np.nonzero(t[:, 0])[0]
+    t0 = t[used, 0].min()
+    us = lambda v: (v - t0) / 100.0  # noqa: E731
+    nsplit = None
+    # attention workgroups: stamp 1 = done (0 if it exited as an inactive split: then = start)
+    nsplit = max(1, min(512 // nkv, 128, (c.max_seq_len + 255) // 256))  # attn_nsplit
+    att = [i for i in used if i < nkv * nsplit]
+    wo = [i for i in used if i >= nkv * nsplit]
+    print(f"workgroups traced: {len(used)} (attention {len(att)}, wo {len(wo)})")
+    if att:
+        a_start = np.array([us(t[i, 0]) for i in att])
+        a_done = np.array([us(t[i, 1]) for i in att if t[i, 1]])
+        print(f"attention start  min {a_start.min():6.2f} max {a_start.max():6.2f} us")
+        if a_done.size:
+            print(f"attention done   min {a_done.min():6.2f} med {np.median(a_done):6.2f} max {a_done.max():6.2f} us")
+        act = [i for i in att if t[i, 5]]
+        for k, name in ((2, "split known"), (3, "scores done"), (6, "softmax done"), (7, "p.V summed"), (4, "p.V reduced"),
+                        (5, "partial drained"), (1, "signalled")):
+            v = np.array([us(t[i, k]) for i in act])
+            if v.size:
+                print(f"  {name:15s} min {v.min():6.2f} med {np.median(v):6.2f} max {v.max():6.2f} us")
+    if wo:
+        for k, name in ((0, "wo start"), (1, "wo passed"), (2, "wo end")):
+            v = np.array([us(t[i, k]) for i in wo])
+            print(f"{name:15s}  min {v.min():6.2f} med {np.median(v):6.2f} max {v.max():6.2f} us")
+    m.close()
+
+
+if __name__ == "__main__":
+    main()

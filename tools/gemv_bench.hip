@@ -76,18 +76,15 @@ int main(int argc, char** argv) {
 
 #define V(NAME, MW, ...) {NAME, [](const Mat& m, const GemvArgs& a) { launch_any<GemvShape<__VA_ARGS__>>(m, a, MW); }}
     std::vector<Variant> vs = {
-        V("t256 r2 u4 nt pf  w4096", 4096, 256, 2, 4, true, 4, true),
-        V("t256 r2 u4 nt --  w4096", 4096, 256, 2, 4, true, 4, false),
-        V("t256 r2 u2 nt pf  w4096", 4096, 256, 2, 2, true, 4, true),
-        V("t256 r2 u2 nt --  w4096", 4096, 256, 2, 2, true, 4, false),
-        V("t256 r4 u2 nt --  w4096", 4096, 256, 4, 2, true, 4, false),
-        V("t256 r2 u4 -- --  w4096", 4096, 256, 2, 4, false, 4, false),
-        V("t256 r2 u8 nt --  w2048 mw2", 2048, 256, 2, 8, true, 2, false),
-        V("t256 r2 u4 nt --  w2048", 2048, 256, 2, 4, true, 4, false),
-        V("t256 r2 u4 nt --  w8192 mw8", 8192, 256, 2, 4, true, 8, false),
         V("t512 r2 u4 nt --  w4096", 4096, 512, 2, 4, true, 4, false),
-        V("t512 r2 u2 nt pf  w4096", 4096, 512, 2, 2, true, 4, true),
-        V("t128 r2 u4 nt --  w4096", 4096, 128, 2, 4, true, 4, false),
+        V("t512 r1 u8 nt --  w4096", 4096, 512, 1, 8, true, 4, false),
+        V("t512 r1 u8 nt pf  w4096", 4096, 512, 1, 8, true, 4, true),
+        V("t512 r1 u4 nt pf  w4096", 4096, 512, 1, 4, true, 4, true),
+        V("t512 r2 u8 nt --  w4096", 4096, 512, 2, 8, true, 4, false),
+        V("t512 r2 u4 nt pf  w4096", 4096, 512, 2, 4, true, 4, true),
+        V("t256 r1 u8 nt --  w4096", 4096, 256, 1, 8, true, 4, false),
+        V("t512 r1 u16 nt -- w2048 mw2", 2048, 512, 1, 16, true, 2, false),
+        V("t512 r2 u8 nt pf  w2048 mw2", 2048, 512, 2, 8, true, 2, true),
     };
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));

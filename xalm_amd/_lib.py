@@ -18,6 +18,9 @@ F32, F16, BF16, F8_E4M3, F8_E5M2, U8, Q8 = 1, 2, 3, 6, 7, 8, 9
 DTYPE_BY_NAME = {"F32": F32, "F16": F16, "BF16": BF16, "F8_E4M3": F8_E4M3, "F8_E5M2": F8_E5M2,
                  "U8": U8, "Q8": Q8}
 DTYPE_SIZE = {F32: 4, F16: 2, BF16: 2, F8_E4M3: 1, F8_E5M2: 1, U8: 1, Q8: 1}
+# enum xh_option
+OPT_FUSE_ATTN_WO = 1
+
 # enum xh_tensor_kind
 EMBED, ATTN_NORM, FFN_NORM, WQ, WK, WV, WO, W1, W2, W3, FINAL_NORM, WCLS = range(12)
 HYDRATE_KV_CACHE, OUTPUT_LOGITS = 0, 1
@@ -64,6 +67,7 @@ _SIGNATURES = {
     "xh_kv_read": (_I, [_P, _I, _I, _I, _I, _P]),
     "xh_active_bytes": (_SZ, [_P, _SZ]),
     "xh_set_graphs": (_I, [_P, _I]),
+    "xh_set_option": (_I, [_P, _I, _I]),
     "xh_op_matmul": (_I, [_P, _P, _P, _I, _I, _I]),
     "xh_op_rmsnorm": (_I, [_P, _P, _P, _I, _I, ctypes.c_float]),
     "xh_op_rope": (_I, [_P, _I, _I, _I, ctypes.c_float, _I]),

@@ -40,12 +40,15 @@ struct AttnArgs {
     const StepParams* sp;
 };
 
-// slots per split for this step: >= ATTN_MIN_T, multiple of 16, nsplit * T >= kv_len
-__device__ __host__ __forceinline__ int attn_split_len(const int kv_len, const int nsplit) {
+// slots per split for this step: >= min_t, multiple of 16, nsplit * T >= kv_len
+__device__ __host__ __forceinline__ int attn_split_len(const int kv_len, const int nsplit,
+                                                       const int min_t = ATTN_MIN_T) {
     int t = (kv_len + nsplit - 1) / nsplit;
     t = (t + 15) & ~15;
-    return t < ATTN_MIN_T ? ATTN_MIN_T : t;
+    return t < min_t ? min_t : t;
 }
+// one round of K/V rows per block: the split floor of a THREADS-thread block
+__device__ __host__ constexpr int attn_min_t(const int hd, const int threads) { return ATTN_PREF * threads / (hd / 8); }
 
 __device__ __forceinline__ float ld_sc1(const float* p) {
     return __builtin_bit_cast(float, __hip_atomic_load((const uint32_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
@@ -54,24 +57,31 @@ __device__ __forceinline__ void st_sc1(float* p, const float v) {
     __hip_atomic_store((uint32_t*)p, __builtin_bit_cast(uint32_t, v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <int HD, int QPK>
-__global__ __launch_bounds__(ATTN_THREADS) void attn_split_kernel(const AttnArgs a) {
+// One workgroup of THREADS threads: KV head g, split s.  PARTIALS (attn_wo.h): every active
+// split stores its partial (o, m, l) write-through, drains, and adds 1 to *done; the
+// consumers merge (no ticket, no merge round trips inside the attention chain).
+template <int HD, int QPK, int THREADS, bool PARTIALS>
+__device__ __forceinline__ void attn_block(const AttnArgs& a, const int g, const int s, char* smem, unsigned* done,
+                                           unsigned long long* dbg = nullptr) {
+#define ATTN_STAMP(k) \
+    do { if (dbg && threadIdx.x == 0) dbg[k] = __builtin_amdgcn_s_memrealtime(); } while (0)
+    constexpr int WAVES = THREADS / 64;
     constexpr int LPR = HD / 8;               // lanes per K/V row (16 B = 8 fp16 each)
-    constexpr int RPP = ATTN_THREADS / LPR;   // rows per pass
+    constexpr int RPP = THREADS / LPR;        // rows per pass
     constexpr int NO = QPK * HD;              // outputs of this block
-    extern __shared__ __attribute__((aligned(16))) char smem[];
     float* red = (float*)smem;                               // [WAVES][NO]
-    float* ml = red + ATTN_WAVES * NO;                       // [QPK][2] (+ flag)
+    float* ml = red + WAVES * NO;                            // [QPK][2] (+ flag)
     float* sc = ml + ((2 * QPK + 4) & ~3);                   // [QPK][T]
     int* flag = (int*)(ml + 2 * QPK);
 
     const int kv_len = a.sp->kv_len;
-    const int T = attn_split_len(kv_len, a.nsplit);
-    const int g = blockIdx.x, s = blockIdx.y;
+    constexpr int MIN_T = PARTIALS ? attn_min_t(HD, THREADS) : ATTN_MIN_T;
+    const int T = attn_split_len(kv_len, a.nsplit, MIN_T);
     const int t0 = s * T;
     if (t0 >= kv_len) return;
     const int t1 = min(kv_len, t0 + T);
     const int n_active = (kv_len + T - 1) / T;
+    ATTN_STAMP(2);
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int sub = tid % LPR, rr = tid / LPR;
     const float scale = 1.0f / sqrtf((float)HD);  // src/infer.cpp:338
@@ -105,8 +115,7 @@ __global__ __launch_bounds__(ATTN_THREADS) void attn_split_kernel(const AttnArgs
             float p = 0.f;
 #pragma unroll
             for (int i = 0; i < 8; i++) p = fmaf(qv[h][i], kf[i], p);
-#pragma unroll
-            for (int o = LPR / 2; o > 0; o >>= 1) p += __shfl_xor(p, o, 64);
+            p = group_reduce<LPR>(p);
             if (sub == 0) sc[h * T + (t - t0)] = p * scale;
         }
     };
@@ -129,10 +138,11 @@ __global__ __launch_bounds__(ATTN_THREADS) void attn_split_kernel(const AttnArgs
         }
     }
     __syncthreads();
+    ATTN_STAMP(3);
 
     // ---- softmax statistics per head (max-subtract + expf, src/infer.cpp:280-297) ----
     const int len = t1 - t0;
-    for (int h = wid; h < QPK; h += ATTN_WAVES) {
+    for (int h = wid; h < QPK; h += WAVES) {
         float m = -FLT_MAX;
         for (int i = lane; i < len; i += 64) m = fmaxf(m, sc[h * T + i]);
         m = wave_max(m);
@@ -146,6 +156,7 @@ __global__ __launch_bounds__(ATTN_THREADS) void attn_split_kernel(const AttnArgs
         if (lane == 0) { ml[2 * h] = m; ml[2 * h + 1] = l; }
     }
     __syncthreads();
+    ATTN_STAMP(6);
 
     // ---- p . V ----
     float acc[QPK][8];
@@ -181,13 +192,13 @@ __global__ __launch_bounds__(ATTN_THREADS) void attn_split_kernel(const AttnArgs
             if (t < t1) pv_row(vv[p], t);
         }
     }
+    ATTN_STAMP(7);
     // reduce over the row slots of this wave (lanes sharing `sub`), then over waves (fixed order)
 #pragma unroll
     for (int h = 0; h < QPK; h++)
 #pragma unroll
         for (int i = 0; i < 8; i++)
-#pragma unroll
-            for (int o = LPR; o < 64; o <<= 1) acc[h][i] += __shfl_xor(acc[h][i], o, 64);
+            acc[h][i] = strided_reduce<LPR>(acc[h][i]);
     if (lane < LPR) {
 #pragma unroll
         for (int h = 0; h < QPK; h++)
@@ -198,12 +209,22 @@ __global__ __launch_bounds__(ATTN_THREADS) void attn_split_kernel(const AttnArgs
     auto block_sum = [&](const int idx) {
         float o = 0.f;
 #pragma unroll
-        for (int w = 0; w < ATTN_WAVES; w++) o += red[w * NO + idx];
+        for (int w = 0; w < WAVES; w++) o += red[w * NO + idx];
         return o;
     };
+    ATTN_STAMP(4);
+    if (PARTIALS) {
+        float* po = a.part_o + ((size_t)s * a.n_heads + g * QPK) * HD;
+        for (int idx = tid; idx < NO; idx += THREADS) st_sc1(po + idx, block_sum(idx));
+        if (tid < 2 * QPK) st_sc1(a.part_ml + ((size_t)s * a.n_heads + g * QPK) * 2 + tid, ml[tid]);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        ATTN_STAMP(5);
+        if (tid == 0) __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
     if (n_active == 1) {
-        for (int idx = tid; idx < NO; idx += ATTN_THREADS)
-            a.out[(size_t)g * NO + idx] = block_sum(idx) / ml[2 * (idx / HD) + 1];
+        for (int idx = tid; idx < NO; idx += THREADS) a.out[(size_t)g * NO + idx] = block_sum(idx) / ml[2 * (idx / HD) + 1];
         return;
     }
 
@@ -213,7 +234,7 @@ __global__ __launch_bounds__(ATTN_THREADS) void attn_split_kernel(const AttnArgs
     // every storing wave drains vmcnt, one lane adds the ticket; the block whose add returns
     // n_active-1 reads every partial with agent-scope relaxed (sc1) loads.  No fences.
     float* po = a.part_o + ((size_t)s * a.n_heads + g * QPK) * HD;
-    for (int idx = tid; idx < NO; idx += ATTN_THREADS) st_sc1(po + idx, block_sum(idx));
+    for (int idx = tid; idx < NO; idx += THREADS) st_sc1(po + idx, block_sum(idx));
     if (tid < 2 * QPK) st_sc1(a.part_ml + ((size_t)s * a.n_heads + g * QPK) * 2 + tid, ml[tid]);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -227,7 +248,7 @@ __global__ __launch_bounds__(ATTN_THREADS) void attn_split_kernel(const AttnArgs
     if (!*flag) return;
     // merge: out = sum_s e^{m_s-M} o_s / sum_s e^{m_s-M} l_s   (per head)
     float* wts = sc;  // [QPK][n_active] weights (sc is free now); den in red[h]
-    for (int h = wid; h < QPK; h += ATTN_WAVES) {
+    for (int h = wid; h < QPK; h += WAVES) {
         float mv[2] = {-FLT_MAX, -FLT_MAX}, lv[2] = {0.f, 0.f};
         int cnt = 0;
         for (int j = lane; j < n_active; j += 64, cnt++) {  // n_active <= 128 -> at most 2 per lane
@@ -247,7 +268,7 @@ __global__ __launch_bounds__(ATTN_THREADS) void attn_split_kernel(const AttnArgs
         if (lane == 0) red[h] = den;
     }
     __syncthreads();
-    for (int idx = tid; idx < NO; idx += ATTN_THREADS) {
+    for (int idx = tid; idx < NO; idx += THREADS) {
         const int h = idx / HD;
         const float* w = wts + h * n_active;
         const float* src = a.part_o + (size_t)g * NO + idx;
@@ -267,10 +288,19 @@ __global__ __launch_bounds__(ATTN_THREADS) void attn_split_kernel(const AttnArgs
     }
 }
 
-// shared-memory bytes of attn_split_kernel<HD,QPK> for a given max split length
-inline size_t attn_smem_bytes(const int hd, const int qpk, const int t_max, const int nsplit) {
+#undef ATTN_STAMP
+
+template <int HD, int QPK>
+__global__ __launch_bounds__(ATTN_THREADS) void attn_split_kernel(const AttnArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    attn_block<HD, QPK, ATTN_THREADS, false>(a, blockIdx.x, blockIdx.y, smem, nullptr);
+}
+
+// shared-memory bytes of attn_block<HD,QPK,threads> for a given max split length
+inline size_t attn_smem_bytes(const int hd, const int qpk, const int t_max, const int nsplit,
+                              const int threads = ATTN_THREADS) {
     const size_t scn = (size_t)qpk * (t_max > nsplit ? t_max : nsplit);
-    return sizeof(float) * ((size_t)ATTN_WAVES * qpk * hd + ((2 * qpk + 4) & ~3) + scn);
+    return sizeof(float) * ((size_t)(threads / 64) * qpk * hd + ((2 * qpk + 4) & ~3) + scn);
 }
 
 }  // namespace xalm

@@ -1,0 +1,179 @@
+// attn_wo.h — attention and the Wo projection (+ residual) in ONE launch.
+//
+// Same math as attn_split_kernel followed by gemv_kernel<PRO_PLAIN, EPI_RESID> (the head loop
+// and output projection of Block::_block_cpu, jubruckne/Xalm src/infer.cpp:434-452), with the
+// launch boundary between them replaced by an in-launch hand-off:
+// * workgroups [0, n_kv_heads * nsplit) are attention workgroups (KV head g = b / nsplit,
+//   split s = b % nsplit; splits past kv_len exit at once).  Every active split stores its
+//   partial (o, m, l) write-through (sc1), drains, and adds 1 to sync[0]: the attention chain
+//   is one K/V round trip plus one publish, with no split waiting on another;
+// * the remaining workgroups own the Wo rows.  Each wave requests its first U weight chunks
+//   (the whole row for f16 / bf16 at d = 4096: the Wo matrix is in flight across the chip)
+//   BEFORE waiting, so the 33.5 MB weight stream overlaps the attention instead of following
+//   it; one lane polls sync[0] until all n_kv_heads * n_active splits are published (relaxed
+//   loads, s_sleep, 2 s bound), then the workgroup merges the partials while staging its x
+//   image (out = sum_s e^{m_s-M} o_s / sum_s e^{m_s-M} l_s, as attention.h's merge) with sc1
+//   loads, and finishes the rows;
+// * the last Wo workgroup to finish zeroes sync[] for the next launch (ticket in sync[1]).
+// Attention workgroups are dispatched first (lowest block ids) and never wait on anything, so
+// progress does not depend on co-residency.  Fan-in: n_kv_heads * n_active arrivals.
+#pragma once
+
+#include "attention.h"
+#include "gemv.h"
+
+namespace xalm {
+
+#ifndef AW_THREADS_OVERRIDE
+constexpr int AW_THREADS = 1024;  // 16 waves: one workgroup per CU at <= 128 VGPRs
+#else
+constexpr int AW_THREADS = AW_THREADS_OVERRIDE;
+#endif
+// Wo shape: 2 rows per wave, a 4096-long f16 / bf16 row (8 KiB) or fp8 row (4 KiB) in U chunks
+template <int DT>
+using AwShape = GemvShape<AW_THREADS, 2, (WDec<DT>::E >= 16 ? 4 : 8), true, 4, true>;
+
+// sync: [0] heads done, [1] Wo workgroups done, [2] timeout flag (sticky, host-checked)
+template <int E>
+__host__ __device__ constexpr size_t aw_image_bytes(const int n) {
+    return (size_t)((n + 64 * E - 1) / (64 * E)) * 64 * E * sizeof(float);
+}
+
+// x image of the Wo rows = the merged attention output.  wts: LDS [n_heads][n_active] weights,
+// [n_heads] denominators, then the (m, l) pairs [n_active][n_heads][2].
+template <int E, int HD>
+__device__ __forceinline__ void aw_stage_merged(const AttnArgs& aa, const int n, const int n_active, float4* xs4,
+                                                float* wts) {
+    const int tid = threadIdx.x;
+    const int nh = aa.n_heads;
+    // (m, l) of every split and head: one batched pass of sc1 loads into LDS ...
+    float* ml = wts + nh * (n_active + 1);
+    for (int i = tid; i < n_active * nh; i += AW_THREADS) {
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)aa.part_ml, 0, 0x7fffffff, 0x00020000);
+        ml[2 * i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, i * 8, 0, 16));  // sc1
+        ml[2 * i + 1] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, i * 8 + 4, 0, 16));
+    }
+    __syncthreads();
+    // ... then per head: weights e^{m_s - M} and the denominator sum_s e^{m_s - M} l_s
+    for (int h = tid; h < nh; h += AW_THREADS) {
+        float M = -FLT_MAX;
+        for (int j = 0; j < n_active; j++) M = fmaxf(M, ml[2 * (j * nh + h)]);
+        float den = 0.f;
+        for (int j = 0; j < n_active; j++) {
+            const float f = expf(ml[2 * (j * nh + h)] - M);
+            wts[h * n_active + j] = f;
+            den = fmaf(f, ml[2 * (j * nh + h) + 1], den);
+        }
+        wts[nh * n_active + h] = den;
+    }
+    __syncthreads();
+    const size_t stride = (size_t)nh * HD;  // floats per split in part_o
+    for (int i = tid; i < (n >> 2); i += AW_THREADS) {
+        const int h = (4 * i) / HD;
+        const float* w = wts + h * n_active;
+        float4 num = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int j = 0; j < n_active; j++) {
+            const u32x4 u = ld_sc1_x4(aa.part_o, (uint32_t)((j * stride + 4 * (size_t)i) * 4));
+            num.x = fmaf(w[j], bits_f32(u.x), num.x);
+            num.y = fmaf(w[j], bits_f32(u.y), num.y);
+            num.z = fmaf(w[j], bits_f32(u.z), num.z);
+            num.w = fmaf(w[j], bits_f32(u.w), num.w);
+        }
+        const float den = wts[nh * n_active + h];
+        const float4 v = make_float4(num.x / den, num.y / den, num.z / den, num.w / den);
+        const int c = i << 2;
+        const int it = c / (64 * E);
+        const int rem = c - it * 64 * E;
+        const int l = rem / E;
+        const int qd = (rem - l * E) >> 2;
+        xs4[(it * (E / 4) + qd) * 64 + l] = v;
+    }
+}
+
+// trace (debug, null = off): per workgroup [8]: start, attention done | hand-off passed, end;
+// attention workgroups also [2] split known, [3] scores done, [4] p.V done, [5] partial drained
+template <int DT, int HD, int QPK>
+__global__ __launch_bounds__(AW_THREADS) void attn_wo_kernel(const AttnArgs aa, const GemvArgs ga,
+                                                                  const int n_kv_heads, unsigned* sync,
+                                                                  unsigned long long* trace) {
+    using S = AwShape<DT>;
+    constexpr int E = WDec<DT>::E;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int n_att = n_kv_heads * aa.nsplit;
+    const int b = blockIdx.x;
+    if (trace && threadIdx.x == 0) trace[8 * b] = __builtin_amdgcn_s_memrealtime();
+    if (b < n_att) {
+        attn_block<HD, QPK, AW_THREADS, true>(aa, b / aa.nsplit, b - (b / aa.nsplit) * aa.nsplit, smem, sync,
+                                              trace ? trace + 8 * b : nullptr);
+        if (trace && threadIdx.x == 0) trace[8 * b + 1] = __builtin_amdgcn_s_memrealtime();
+        return;
+    }
+    float* red = (float*)smem;
+    float4* xs4 = (float4*)(smem + LDS_HEAD_BYTES);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int nb = gridDim.x - n_att;
+    const int g = (b - n_att) * S::WAVES + wid;
+    auto wait_heads = [&]() {
+        const int kv_len = aa.sp->kv_len;
+        const int T = attn_split_len(kv_len, aa.nsplit, attn_min_t(HD, AW_THREADS));
+        const int n_active = (kv_len + T - 1) / T;
+        if (threadIdx.x == 0) {
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            const unsigned target = (unsigned)(n_kv_heads * n_active);
+            while (__hip_atomic_load(sync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+                __builtin_amdgcn_s_sleep(1);
+                if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {  // 2 s at 100 MHz: flag, go on
+                    __hip_atomic_store(sync + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    break;
+                }
+            }
+        }
+        __syncthreads();
+        if (trace && threadIdx.x == 0) trace[8 * b + 1] = __builtin_amdgcn_s_memrealtime();
+        aw_stage_merged<E, HD>(aa, ga.n, n_active, xs4, (float*)(smem + LDS_HEAD_BYTES + aw_image_bytes<E>(ga.n)));
+        __syncthreads();
+    };
+    const int n_groups = gemv_groups<S>(ga);
+    if (ga.n == S::U * 64 * E && n_groups <= nb * S::WAVES) {
+        // every wave owns at most one group and its whole rows fit the U chunks: request them,
+        // then wait; nothing but the dot products is left after the hand-off
+        u32x4 w[S::U][S::ROWS];
+        if (g < n_groups && !(ga.act & 256)) gemv_prefetch<S>(ga, g, lane, w);
+        wait_heads();
+        if (g < n_groups && (ga.act & 256)) gemv_prefetch<S>(ga, g, lane, w);
+        if (g < n_groups) {
+            float acc[S::ROWS];
+#pragma unroll
+            for (int r = 0; r < S::ROWS; r++) acc[r] = 0.f;
+            gemv_compute<DT, S::ROWS, S::U>(w, xs4, 0, lane, acc);
+#pragma unroll
+            for (int r = 0; r < S::ROWS; r++) acc[r] = wave_sum(acc[r]);
+            if (lane == 0) gemv_epilogue<EPI_RESID, S::ROWS>(ga, g * S::ROWS, acc);
+        }
+    } else {
+        using G = GemvShape<AW_THREADS, S::ROWS, 4, true, 4, false>;
+        wait_heads();
+        u32x4 none[G::U][G::ROWS];
+        gemv_rows<DT, EPI_RESID, G>(ga, g, nb * S::WAVES, lane, xs4, none, false);
+    }
+    __syncthreads();
+    if (trace && threadIdx.x == 0) trace[8 * b + 2] = __builtin_amdgcn_s_memrealtime();
+    if (threadIdx.x == 0) {
+        const unsigned c = __hip_atomic_fetch_add(sync + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (c == (unsigned)nb - 1) {
+            __hip_atomic_store(sync, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(sync + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
+// LDS bytes: the larger of the attention tiles (at AW_THREADS) and the Wo x image
+template <int DT>
+inline size_t attn_wo_smem_bytes(const int hd, const int qpk, const int t_max, const int nsplit, const int q_dim,
+                                 const int n_heads) {
+    const size_t att = attn_smem_bytes(hd, qpk, t_max, nsplit, AW_THREADS);
+    const size_t wo = LDS_HEAD_BYTES + aw_image_bytes<WDec<DT>::E>(q_dim) + sizeof(float) * (size_t)n_heads * (3 * nsplit + 1);
+    return att > wo ? att : wo;
+}
+
+}  // namespace xalm

@@ -130,16 +130,56 @@ __device__ __forceinline__ float f16_bits_to_f32(const uint16_t h) {
     return (float)__builtin_bit_cast(_Float16, h);
 }
 
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+// ---- cross-lane reductions without LDS: DPP within 16-lane rows, permlane swaps across rows
+// (v_permlane16/32_swap, gfx950; hipcc inserts the VALU->permlane wait states).  Every lane of
+// the reduced group ends with the same value.
+enum { DPP_XOR1 = 0xB1, DPP_XOR2 = 0x4E, DPP_ROW_ROR = 0x120, DPP_ROW_MIRROR = 0x140, DPP_ROW_HALF_MIRROR = 0x141 };
+template <int CTRL>
+__device__ __forceinline__ float dpp(const float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+struct OpSum { __device__ static float f(float a, float b) { return a + b; } };
+struct OpMax { __device__ static float f(float a, float b) { return fmaxf(a, b); } };
+// combine the two rows of each row pair (1 with 0, 3 with 2) / the two half-waves
+// The swaps are inline asm: hipcc (ROCm 7.2) takes the builtins' second result from the
+// first operand's register (measured: permlane16_swap(x, y)[1] came back equal to [0]).  The
+// s_nop 1 covers the "VALU write -> v_permlane read" hazard (cdna_hip_programming.md T21).
+template <class Op>
+__device__ __forceinline__ float rows_pair(const float v) {
+    float a = v, b = v;
+    asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+    return Op::f(a, b);
+}
+template <class Op>
+__device__ __forceinline__ float halves(const float v) {
+    float a = v, b = v;
+    asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+    return Op::f(a, b);
+}
+// over aligned groups of G consecutive lanes (G = 2, 4, ..., 64)
+template <int G, class Op = OpSum>
+__device__ __forceinline__ float group_reduce(float v) {
+    if (G >= 2) v = Op::f(v, dpp<DPP_XOR1>(v));
+    if (G >= 4) v = Op::f(v, dpp<DPP_XOR2>(v));
+    if (G >= 8) v = Op::f(v, dpp<DPP_ROW_HALF_MIRROR>(v));
+    if (G >= 16) v = Op::f(v, dpp<DPP_ROW_MIRROR>(v));
+    if (G >= 32) v = rows_pair<Op>(v);
+    if (G >= 64) v = halves<Op>(v);
     return v;
 }
-__device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+// over the 64 / S lanes congruent mod S (S = 1, 2, 4, ..., 32): lanes l, l+S, l+2S, ...
+template <int S, class Op = OpSum>
+__device__ __forceinline__ float strided_reduce(float v) {
+    if (S <= 1) v = Op::f(v, dpp<DPP_ROW_ROR + 1>(v));
+    if (S <= 2) v = Op::f(v, dpp<DPP_ROW_ROR + 2>(v));
+    if (S <= 4) v = Op::f(v, dpp<DPP_ROW_ROR + 4>(v));
+    if (S <= 8) v = Op::f(v, dpp<DPP_ROW_ROR + 8>(v));
+    if (S <= 16) v = rows_pair<Op>(v);
+    v = halves<Op>(v);
     return v;
 }
+__device__ __forceinline__ float wave_sum(float v) { return group_reduce<64, OpSum>(v); }
+__device__ __forceinline__ float wave_max(float v) { return group_reduce<64, OpMax>(v); }
 
 // Per-token dynamic scalars, read by every kernel of a captured graph.
 // kv_sink / kv_pos / kv_len follow src/infer.cpp:611-613.
@@ -161,6 +201,12 @@ __device__ __forceinline__ void step_positions(StepParams* sp, const int pos) {
     sp->kv_sink = kv_sink;
     sp->kv_pos = kv_sink + (pos - kv_sink) % (msl - kv_sink);
     sp->kv_len = pos >= msl ? msl : pos + 1;
+}
+
+// 16-byte sc1 load through a buffer descriptor (aux 16 = sc1, cdna_hip_programming.md T8 / G16)
+__device__ __forceinline__ u32x4 ld_sc1_x4(const void* base, const uint32_t byte_off) {
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, 0x7fffffff, 0x00020000);
+    return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)byte_off, 0, 16));
 }
 
 }  // namespace xalm

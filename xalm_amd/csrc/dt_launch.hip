@@ -1,9 +1,10 @@
-// pk_launch.hip — persistent-kernel instantiations for one weight dtype (-DPK_DT=<xh_dtype>).
+// dt_launch.hip — persistent-kernel and fused attention + Wo instantiations for one weight
+// dtype (-DPK_DT=<xh_dtype>).
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
 
-#include "pk_launch.h"
+#include "dt_launch.h"
 
 #ifndef PK_DT
 #error "compile with -DPK_DT=<xh_dtype id>"
@@ -58,10 +59,39 @@ int unsupported(int dt, int dtc, char* err, size_t errlen) {
     return XH_E_INVALID;
 }
 
+template <int DT, int HD, int QPK>
+int aw_go(const AttnArgs& aa, const GemvArgs& ga, int n_kv_heads, int t_max, unsigned* sync, int max_waves,
+          hipStream_t stream, unsigned long long* trace) {
+    using S = AwShape<DT>;
+    const size_t smem = attn_wo_smem_bytes<DT>(HD, QPK, t_max, aa.nsplit, ga.n, aa.n_heads);
+    if (smem > 160 * 1024) return XH_E_INVALID;
+    auto k = attn_wo_kernel<DT, HD, QPK>;
+    static bool attr = false;
+    if (!attr) {
+        if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
+            return XH_E_HIP;
+        attr = true;
+    }
+    const int blocks = n_kv_heads * aa.nsplit + gemv_blocks<S>(ga.rows, max_waves / S::WAVES);
+    hipLaunchKernelGGL(k, dim3(blocks), dim3(AW_THREADS), smem, stream, aa, ga, n_kv_heads, sync, trace);
+    return hipGetLastError() == hipSuccess ? 0 : XH_E_HIP;
+}
+
 }  // namespace
 
 #define XALM_CAT2(a, b) a##b
 #define XALM_CAT(a, b) XALM_CAT2(a, b)
+int XALM_CAT(aw_launch_dt, PK_DT)(const AttnArgs& aa, const GemvArgs& ga, int head_dim, int qpk, int n_kv_heads,
+                                  int t_max, unsigned* sync, int max_waves, hipStream_t stream,
+                                  unsigned long long* trace) {
+    if (head_dim == 128 && qpk == 4) return aw_go<PK_DT, 128, 4>(aa, ga, n_kv_heads, t_max, sync, max_waves, stream, trace);
+    if (head_dim == 128 && qpk == 8) return aw_go<PK_DT, 128, 8>(aa, ga, n_kv_heads, t_max, sync, max_waves, stream, trace);
+    if (head_dim == 64 && qpk == 4) return aw_go<PK_DT, 64, 4>(aa, ga, n_kv_heads, t_max, sync, max_waves, stream, trace);
+    if (head_dim == 16 && qpk == 2) return aw_go<PK_DT, 16, 2>(aa, ga, n_kv_heads, t_max, sync, max_waves, stream, trace);
+    return XH_E_INVALID;
+}
+
+#if PK_DT != 9  // no persistent engine for Q8
 int XALM_CAT(pk_launch_dt, PK_DT)(const PkArgs& a, int dtc, int n_cu, hipStream_t stream, char* err, size_t errlen) {
 #if PK_DT == 6 || PK_DT == 7  // fp8 matrices: lm_head bf16 (convert.py) or fp8
     if (dtc == XH_BF16) return go_hd<PK_DT, XH_BF16>(a, n_cu, stream, err, errlen);
@@ -69,5 +99,6 @@ int XALM_CAT(pk_launch_dt, PK_DT)(const PkArgs& a, int dtc, int n_cu, hipStream_
     if (dtc == PK_DT) return go_hd<PK_DT, PK_DT>(a, n_cu, stream, err, errlen);
     return unsupported(PK_DT, dtc, err, errlen);
 }
+#endif
 
 }  // namespace xalm

@@ -116,14 +116,21 @@ __device__ __forceinline__ float4 load_norm4(const void* w, const int dtype, con
 
 // x (optionally rms-normalised and weighted) -> LDS image xs4, permuted so that lane l at
 // chunk `it` finds the E/4 float4 it multiplies at xs4[(it*E/4 + q)*64 + l].
-template <int E, int PRO, int THREADS>
+// SC1: x was published inside the running launch (write-through): read it with sc1 loads.
+template <int E, int PRO, int THREADS, bool SC1 = false>
 __device__ __forceinline__ void stage_x(const GemvArgs& a, float4* xs4, float* red) {
     const int n = a.n;
     float scale = 1.f;
     if (PRO == PRO_RMSNORM) scale = block_rms_scale<THREADS>(a.x, n, a.eps, red);
     const float4* x4 = (const float4*)a.x;
     for (int i = threadIdx.x; i < (n >> 2); i += THREADS) {
-        float4 v = x4[i];
+        float4 v;
+        if (SC1) {
+            const u32x4 u = ld_sc1_x4(a.x, (uint32_t)i * 16);
+            v = make_float4(bits_f32(u.x), bits_f32(u.y), bits_f32(u.z), bits_f32(u.w));
+        } else {
+            v = x4[i];
+        }
         if (PRO == PRO_RMSNORM) {
             const float4 w = load_norm4(a.norm_w, a.norm_dtype, i);
             v.x = v.x * scale * w.x;  // x[i] * scale * weight[i], src/infer.cpp:234
@@ -246,51 +253,41 @@ __device__ __forceinline__ void gemv_chunk(const char* wrow, const size_t row_by
     gemv_compute<DT, ROWS, U>(wv, xs4, it, lane, acc);
 }
 
-// Grid: every wave owns the same number of ROWS-row groups (g = wave, wave + W, ...), so no
-// wave is left with a partial last round.  The first U weight chunks of the first group are
-// requested before the x image is staged, so HBM latency overlaps the prologue.
-template <int DT, int PRO, int EPI, class S>
-__global__ __launch_bounds__(S::THREADS, S::MINW) void gemv_kernel(const GemvArgs a) {
-    constexpr int ROWS = S::ROWS, U = S::U;
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    float* red = (float*)smem;
-    float4* xs4 = (float4*)(smem + LDS_HEAD_BYTES);
-    constexpr int E = WDec<DT>::E;
-    const int lane = threadIdx.x & 63;
-    const int wid = threadIdx.x >> 6;
+// Row group `grp` of the matrix: lane pointer and row stride (0 for the duplicated last row
+// of an odd row count: rows past the end re-read the last row and are never stored).
+template <int ROWS>
+__device__ __forceinline__ const char* gemv_row_ptr(const GemvArgs& a, const int grp, const int lane, size_t& rstride) {
+    const int rmax = a.rows - 1;
+    const int row0 = grp * ROWS;
+    rstride = (row0 + ROWS - 1 <= rmax) ? a.row_bytes : 0;
+    return (const char*)a.w + (size_t)(row0 < rmax ? row0 : rmax) * a.row_bytes + lane * 16;
+}
+template <class S>
+__device__ __forceinline__ int gemv_groups(const GemvArgs& a) { return (a.rows + S::ROWS - 1) / S::ROWS; }
 
+// chunks [0, U) of group g into pre (the caller checked g < groups and n_full >= U)
+template <class S>
+__device__ __forceinline__ void gemv_prefetch(const GemvArgs& a, const int g, const int lane,
+                                              u32x4 (&pre)[S::U][S::ROWS]) {
+    size_t rs;
+    const char* wrow = gemv_row_ptr<S::ROWS>(a, g, lane, rs);
+    gemv_load<S::ROWS, S::U, S::NT>(pre, wrow, rs, 0);
+}
+
+// Groups g, g + total_waves, ... of this wave against the staged x image; the first group
+// starts from `pre` when `first` (its chunks [0, U) already requested).
+template <int DT, int EPI, class S>
+__device__ __forceinline__ void gemv_rows(const GemvArgs& a, int g, const int total_waves, const int lane,
+                                          const float4* xs4, const u32x4 (&pre)[S::U][S::ROWS], bool first) {
+    constexpr int ROWS = S::ROWS, U = S::U;
+    constexpr int E = WDec<DT>::E;
     const int n = a.n;
     const int n_full = n / (64 * E);
     const int n_it = (n + 64 * E - 1) / (64 * E);
-    const int n_groups = (a.rows + ROWS - 1) / ROWS;
-    const int total_waves = gridDim.x * S::WAVES;
-    const int rmax = a.rows - 1;
-    const size_t rb = a.row_bytes;
-    int g = blockIdx.x * S::WAVES + wid;
-
-    // rows past the end (odd vocab) re-read the last row and are never stored
-    auto row_ptr = [&](int grp, size_t& rstride) {
-        const int row0 = grp * ROWS;
-        rstride = (row0 + ROWS - 1 <= rmax) ? rb : 0;
-        return (const char*)a.w + (size_t)(row0 < rmax ? row0 : rmax) * rb + lane * 16;
-    };
-
-    u32x4 pre[U][ROWS];
-    const bool prefetched = S::PF && g < n_groups && n_full >= U;
-    if (prefetched) {
-        size_t rs;
-        const char* wrow = row_ptr(g, rs);
-        gemv_load<ROWS, U, S::NT>(pre, wrow, rs, 0);
-    }
-
-    stage_x<E, PRO, S::THREADS>(a, xs4, red);
-    if (EPI == EPI_QKV && blockIdx.x == 0) rotate_sinks<S::THREADS>(a, a.sp->kv_sink);
-    __syncthreads();
-
-    bool first = prefetched;
+    const int n_groups = gemv_groups<S>(a);
     for (; g < n_groups; g += total_waves) {
         size_t rstride;
-        const char* wrow = row_ptr(g, rstride);
+        const char* wrow = gemv_row_ptr<ROWS>(a, g, lane, rstride);
         float acc[ROWS];
 #pragma unroll
         for (int r = 0; r < ROWS; r++) acc[r] = 0.f;
@@ -309,6 +306,31 @@ __global__ __launch_bounds__(S::THREADS, S::MINW) void gemv_kernel(const GemvArg
         for (int r = 0; r < ROWS; r++) acc[r] = wave_sum(acc[r]);
         if (lane == 0) gemv_epilogue<EPI, ROWS>(a, g * ROWS, acc);
     }
+}
+
+// Grid: every wave owns the same number of ROWS-row groups (g = wave, wave + W, ...), so no
+// wave is left with a partial last round.  The first U weight chunks of the first group are
+// requested before the x image is staged, so HBM latency overlaps the prologue.
+template <int DT, int PRO, int EPI, class S>
+__global__ __launch_bounds__(S::THREADS, S::MINW) void gemv_kernel(const GemvArgs a) {
+    constexpr int ROWS = S::ROWS, U = S::U;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    float* red = (float*)smem;
+    float4* xs4 = (float4*)(smem + LDS_HEAD_BYTES);
+    constexpr int E = WDec<DT>::E;
+    const int lane = threadIdx.x & 63;
+    const int wid = threadIdx.x >> 6;
+
+    const int g = blockIdx.x * S::WAVES + wid;
+
+    const bool prefetched = S::PF && g < gemv_groups<S>(a) && a.n / (64 * E) >= U;
+    u32x4 pre[U][ROWS];
+    if (prefetched) gemv_prefetch<S>(a, g, lane, pre);
+
+    stage_x<E, PRO, S::THREADS>(a, xs4, red);
+    if (EPI == EPI_QKV && blockIdx.x == 0) rotate_sinks<S::THREADS>(a, a.sp->kv_sink);
+    __syncthreads();
+    gemv_rows<DT, EPI, S>(a, g, gridDim.x * S::WAVES, lane, xs4, pre, prefetched);
 }
 
 // LDS bytes and grid of one launch

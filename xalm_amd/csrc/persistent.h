@@ -95,11 +95,6 @@ __device__ __forceinline__ uint32_t ld_sc1_u32(const void* p) {
 __device__ __forceinline__ float ld_sc1_f(const float* p) { return __builtin_bit_cast(float, ld_sc1_u32(p)); }
 __device__ __forceinline__ void st_sc1_f(float* p, float v) { st_sc1_u32(p, __builtin_bit_cast(uint32_t, v)); }
 
-// 16-byte sc1 load through a buffer descriptor (aux 16 = sc1, cdna_hip_programming.md T8 / G16)
-__device__ __forceinline__ u32x4 ld_sc1_x4(const void* base, const uint32_t byte_off) {
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, 0x7fffffff, 0x00020000);
-    return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)byte_off, 0, 16));
-}
 
 // threadIdx.x behind an empty asm: thread-derived addresses are recomputed where they are
 // used instead of being hoisted out of the token/layer loops and kept live (they spilled)
@@ -349,8 +344,7 @@ __device__ __forceinline__ void pk_attention(const PkArgs& a, const PkLayer& ly,
                     float pr = 0.f;
 #pragma unroll
                     for (int i = 0; i < 8; i++) pr = fmaf(qv[h][i], kf[i], pr);
-#pragma unroll
-                    for (int o = LPR / 2; o > 0; o >>= 1) pr += __shfl_xor(pr, o, 64);
+                    pr = group_reduce<LPR>(pr);
                     if (sub == 0) sc[h * T + (t - t0)] = pr * scale;
                 }
             }
@@ -403,8 +397,7 @@ __device__ __forceinline__ void pk_attention(const PkArgs& a, const PkLayer& ly,
     for (int h = 0; h < QPK; h++)
 #pragma unroll
         for (int i = 0; i < 8; i++)
-#pragma unroll
-            for (int o = LPR; o < 64; o <<= 1) acc[h][i] += __shfl_xor(acc[h][i], o, 64);
+            acc[h][i] = strided_reduce<LPR>(acc[h][i]);
     if (lane < LPR) {
 #pragma unroll
         for (int h = 0; h < QPK; h++)

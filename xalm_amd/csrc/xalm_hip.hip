@@ -28,7 +28,7 @@
 #include "../../include/xalm_synth.h"
 #include "attention.h"
 #include "gemv.h"
-#include "pk_launch.h"
+#include "dt_launch.h"
 #include "standalone.h"
 
 using namespace xalm;
@@ -84,6 +84,10 @@ struct xh_ctx {
     int* dec_tokens = nullptr;      // device, decode loop output
     int dec_cap = 0;
     int nsplit = 1, t_max = 16;
+    // fused attention + Wo launch (attn_wo.h): per-layer hand-off words [n_layers][4]
+    bool fuse_attn_wo = true;
+    unsigned* aw_sync = nullptr;
+    int t_max_aw = 16;
     bool use_graphs = true;
     hipGraphExec_t g_logits = nullptr, g_hydrate = nullptr, g_decode = nullptr;
     int max_gemv_waves = 4096;  // 16 waves per CU
@@ -103,6 +107,7 @@ struct xh_ctx {
     float pk_last_us = 0.f;
     unsigned long long* pk_trace = nullptr;  // device [PK_TRACE_WG][pk_trace_len]
     bool pk_trace_on = false;
+    bool aw_trace_on = false;  // fused attention + Wo launches write pk_trace (debug)
 
     uint16_t* kcache(int l) { return kv + (size_t)l * 2 * c.max_seq_len * kv_dim; }
     uint16_t* vcache(int l) { return kcache(l) + (size_t)c.max_seq_len * kv_dim; }
@@ -305,6 +310,40 @@ __global__ void argmax_advance_kernel(const float* logits, int vocab, StepParams
     }
 }
 
+bool use_attn_wo(const xh_ctx* ctx, int l) {
+    const int dt = ctx->L[l].wo_dt;
+    return ctx->fuse_attn_wo && aw_instantiated(ctx->c.head_dim, ctx->qpk) &&
+           (dt == XH_F32 || dt == XH_F16 || dt == XH_BF16 || dt == XH_F8_E4M3 || dt == XH_F8_E5M2 || dt == XH_Q8);
+}
+
+int launch_attn_wo(xh_ctx* ctx, int l, hipStream_t s) {
+    const AttnArgs aa = attn_args(ctx, l);
+    GemvArgs ga = wo_args(ctx, l);
+    if (getenv("XH_AW_NOPF")) ga.act |= 256;  // experiment: Wo loads after the hand-off
+    unsigned* sync = ctx->aw_sync + 4 * l;
+    const int hd = ctx->c.head_dim, qpk = ctx->qpk, nkv = ctx->c.n_kv_heads, tm = ctx->t_max_aw;
+    const int mw = ctx->max_gemv_waves;
+    switch (ctx->L[l].wo_dt) {
+        case XH_F32: return aw_launch_dt1(aa, ga, hd, qpk, nkv, tm, sync, mw, s, ctx->aw_trace_on ? ctx->pk_trace : nullptr);
+        case XH_F16: return aw_launch_dt2(aa, ga, hd, qpk, nkv, tm, sync, mw, s, ctx->aw_trace_on ? ctx->pk_trace : nullptr);
+        case XH_BF16: return aw_launch_dt3(aa, ga, hd, qpk, nkv, tm, sync, mw, s, ctx->aw_trace_on ? ctx->pk_trace : nullptr);
+        case XH_F8_E4M3: return aw_launch_dt6(aa, ga, hd, qpk, nkv, tm, sync, mw, s, ctx->aw_trace_on ? ctx->pk_trace : nullptr);
+        case XH_F8_E5M2: return aw_launch_dt7(aa, ga, hd, qpk, nkv, tm, sync, mw, s, ctx->aw_trace_on ? ctx->pk_trace : nullptr);
+        case XH_Q8: return aw_launch_dt9(aa, ga, hd, qpk, nkv, tm, sync, mw, s, ctx->aw_trace_on ? ctx->pk_trace : nullptr);
+        default: return XH_E_INVALID;
+    }
+}
+
+// a fused hand-off that timed out leaves its sticky flag: report it (after the stream sync)
+int check_aw(xh_ctx* ctx) {
+    if (!ctx->fuse_attn_wo) return 0;
+    std::vector<unsigned> h((size_t)ctx->c.n_layers * 4);
+    HIP_TRY(ctx, hipMemcpy(h.data(), ctx->aw_sync, h.size() * sizeof(unsigned), hipMemcpyDeviceToHost));
+    for (int l = 0; l < ctx->c.n_layers; l++)
+        if (h[4 * l + 2]) return set_err(ctx, XH_E_HIP, "layer %d: attention -> Wo hand-off timed out", l);
+    return 0;
+}
+
 int enqueue_step(xh_ctx* ctx, hipStream_t s, bool with_logits) {
     const xh_config& c = ctx->c;
     const int mb = ctx->max_gemv_waves;
@@ -314,10 +353,15 @@ int enqueue_step(xh_ctx* ctx, hipStream_t s, bool with_logits) {
         const LayerW& w = ctx->L[l];
         if (!launch_gemv<PRO_RMSNORM, EPI_QKV>(w.qkv_dt, qkv_args(ctx, l), s, mb))
             return set_err(ctx, XH_E_INVALID, "layer %d: unsupported qkv dtype %d", l, w.qkv_dt);
-        if (!launch_attn(attn_args(ctx, l), c.head_dim, ctx->qpk, c.n_kv_heads, ctx->t_max, s))
-            return set_err(ctx, XH_E_INVALID, "unsupported head_dim %d / q-per-kv %d", c.head_dim, ctx->qpk);
-        if (!launch_gemv<PRO_PLAIN, EPI_RESID>(w.wo_dt, wo_args(ctx, l), s, mb))
-            return set_err(ctx, XH_E_INVALID, "layer %d: unsupported wo dtype", l);
+        if (use_attn_wo(ctx, l)) {
+            const int rc = launch_attn_wo(ctx, l, s);
+            if (rc) return set_err(ctx, rc, "layer %d: fused attention + Wo launch failed", l);
+        } else {
+            if (!launch_attn(attn_args(ctx, l), c.head_dim, ctx->qpk, c.n_kv_heads, ctx->t_max, s))
+                return set_err(ctx, XH_E_INVALID, "unsupported head_dim %d / q-per-kv %d", c.head_dim, ctx->qpk);
+            if (!launch_gemv<PRO_PLAIN, EPI_RESID>(w.wo_dt, wo_args(ctx, l), s, mb))
+                return set_err(ctx, XH_E_INVALID, "layer %d: unsupported wo dtype", l);
+        }
         if (!launch_gemv<PRO_RMSNORM, EPI_GLU>(w.w13_dt, w13_args(ctx, l), s, mb))
             return set_err(ctx, XH_E_INVALID, "layer %d: unsupported w1/w3 dtype", l);
         if (!launch_gemv<PRO_PLAIN, EPI_RESID>(w.w2_dt, w2_args(ctx, l), s, mb))
@@ -554,6 +598,7 @@ int xh_create(const xh_config* cfg, int device_ordinal, xh_ctx** out) {
     ctx->qpk = qpk;
     ctx->nsplit = attn_nsplit(c.n_kv_heads, c.max_seq_len);
     ctx->t_max = attn_split_len(c.max_seq_len, ctx->nsplit);
+    ctx->t_max_aw = attn_split_len(c.max_seq_len, ctx->nsplit, attn_min_t(c.head_dim, AW_THREADS));
     int rc = 0;
 #define CREATE_TRY(expr) do { rc = (expr); if (rc) { g_create_error = ctx->err; xh_destroy(ctx); return rc; } } while (0)
     if (hipSetDevice(device_ordinal) != hipSuccess) { delete ctx; return set_err(nullptr, XH_E_HIP, "hipSetDevice failed"); }
@@ -570,6 +615,7 @@ int xh_create(const xh_config* cfg, int device_ordinal, xh_ctx** out) {
     CREATE_TRY(dmalloc(ctx, &ctx->part_o, (size_t)ctx->nsplit * ctx->q_dim));
     CREATE_TRY(dmalloc(ctx, &ctx->part_ml, (size_t)ctx->nsplit * c.n_heads * 2));
     CREATE_TRY(dmalloc(ctx, &ctx->attn_cnt, (size_t)c.n_kv_heads));
+    CREATE_TRY(dmalloc(ctx, &ctx->aw_sync, (size_t)c.n_layers * 4));
     {
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, device_ordinal) != hipSuccess) {
@@ -585,7 +631,8 @@ int xh_create(const xh_config* cfg, int device_ordinal, xh_ctx** out) {
     CREATE_TRY(dmalloc(ctx, &ctx->pk_tickets, (size_t)c.n_kv_heads));
     CREATE_TRY(dmalloc(ctx, &ctx->pk_err, 2));
     CREATE_TRY(dmalloc(ctx, &ctx->pk_cand, (size_t)ctx->n_cu));
-    CREATE_TRY(dmalloc(ctx, &ctx->pk_trace, (size_t)PK_TRACE_WG * pk_trace_len(c.n_layers)));
+    CREATE_TRY(dmalloc(ctx, &ctx->pk_trace, std::max<size_t>((size_t)PK_TRACE_WG * pk_trace_len(c.n_layers),
+                                                             8 * ((size_t)c.n_kv_heads * ctx->nsplit + 4096))));
     CREATE_TRY(dmalloc(ctx, &ctx->pk_prompt, (size_t)ctx->pk_prompt_cap));
     if (hipHostMalloc((void**)&ctx->pk_host, (2 + (size_t)ctx->pk_prompt_cap) * sizeof(int), hipHostMallocDefault) !=
         hipSuccess) {
@@ -644,7 +691,7 @@ void xh_destroy(xh_ctx* ctx) {
     if (ctx->wcls && ctx->wcls != ctx->embed) hipFree(ctx->wcls);
     hipFree(ctx->embed); hipFree(ctx->final_norm);
     hipFree(ctx->kv); hipFree(ctx->x); hipFree(ctx->q); hipFree(ctx->attn_out); hipFree(ctx->hb);
-    hipFree(ctx->logits); hipFree(ctx->part_o); hipFree(ctx->part_ml); hipFree(ctx->attn_cnt); hipFree(ctx->rope_freq);
+    hipFree(ctx->logits); hipFree(ctx->part_o); hipFree(ctx->part_ml); hipFree(ctx->attn_cnt); hipFree(ctx->aw_sync); hipFree(ctx->rope_freq);
     hipFree(ctx->pk_layers); hipFree(ctx->pk_counters); hipFree(ctx->pk_tickets); hipFree(ctx->pk_err);
     hipFree(ctx->pk_cand); hipFree(ctx->pk_prompt); hipFree(ctx->pk_trace);
     if (ctx->pk_host) hipHostFree(ctx->pk_host);
@@ -844,7 +891,7 @@ int xh_forward(xh_ctx* ctx, int token, int pos, int mode, float* logits_out) {
         HIP_TRY(ctx, hipMemcpyAsync(logits_out, ctx->logits, (size_t)ctx->c.vocab_size * 4, hipMemcpyDeviceToHost,
                                     ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-    return 0;
+    return check_aw(ctx);
 }
 
 int xh_decode_greedy(xh_ctx* ctx, int pos, int n_steps, int stop_a, int stop_b, int* tokens_out, int* n_done) {
@@ -900,7 +947,7 @@ int xh_decode_greedy(xh_ctx* ctx, int pos, int n_steps, int stop_a, int stop_b, 
                                     ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     if (n_done) *n_done = done;
-    return 0;
+    return check_aw(ctx);
 }
 
 int xh_get_logits(xh_ctx* ctx, float* logits_out) {
@@ -991,7 +1038,7 @@ int xh_prefill(xh_ctx* ctx, const int* tokens, int n, int pos0, int want_logits,
         HIP_TRY(ctx, hipMemcpyAsync(logits_out, ctx->logits, (size_t)ctx->c.vocab_size * 4, hipMemcpyDeviceToHost,
                                     ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-    return 0;
+    return check_aw(ctx);
 }
 
 int xh_set_engine(xh_ctx* ctx, int engine) {
@@ -1013,14 +1060,16 @@ int xh_last_launch_us(const xh_ctx* ctx, float* us) {
 
 int xh_debug_trace(xh_ctx* ctx, int enable, uint64_t* out, int cap, int* len) {
     if (!ctx) return XH_E_INVALID;
-    const int n = PK_TRACE_WG * pk_trace_len(ctx->c.n_layers);
+    const int n = std::max(PK_TRACE_WG * pk_trace_len(ctx->c.n_layers), 8 * (ctx->c.n_kv_heads * ctx->nsplit + 4096));
     if (len) *len = n;
     if (out && cap > 0) {
         HIP_TRY(ctx, hipSetDevice(ctx->dev));
         HIP_TRY(ctx, hipMemcpy(out, ctx->pk_trace, (size_t)std::min(cap, n) * sizeof(uint64_t), hipMemcpyDeviceToHost));
     }
     if (enable >= 0) {
-        ctx->pk_trace_on = enable != 0;
+        ctx->pk_trace_on = (enable & 1) != 0;
+        ctx->aw_trace_on = (enable & 2) != 0;
+        drop_graphs(ctx);
         HIP_TRY(ctx, hipMemset(ctx->pk_trace, 0, (size_t)n * sizeof(uint64_t)));
     }
     return 0;
@@ -1029,6 +1078,17 @@ int xh_debug_trace(xh_ctx* ctx, int enable, uint64_t* out, int cap, int* len) {
 int xh_get_engine(const xh_ctx* ctx) {
     if (!ctx) return -1;
     return use_persistent(const_cast<xh_ctx*>(ctx)) ? 1 : 0;
+}
+
+int xh_set_option(xh_ctx* ctx, int option, int value) {
+    if (!ctx) return XH_E_INVALID;
+    switch (option) {
+        case XH_OPT_FUSE_ATTN_WO:
+            ctx->fuse_attn_wo = value != 0;
+            drop_graphs(ctx);
+            return 0;
+        default: return set_err(ctx, XH_E_INVALID, "unknown option %d", option);
+    }
 }
 
 int xh_set_graphs(xh_ctx* ctx, int enable) {

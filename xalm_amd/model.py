@@ -123,6 +123,9 @@ class Model:
     def set_graphs(self, enable: bool):
         L.check(L.lib().xh_set_graphs(self._ctx, int(enable)), self._ctx)
 
+    def set_option(self, option: int, value: int):
+        L.check(L.lib().xh_set_option(self._ctx, int(option), int(value)), self._ctx)
+
     def active_bytes(self, pos: int) -> int:
         return int(L.lib().xh_active_bytes(self._ctx, pos))
 
