@@ -51,7 +51,7 @@ def main():
             if v.size:
                 print(f"  {name:15s} min {v.min():6.2f} med {np.median(v):6.2f} max {v.max():6.2f} us")
     if wo:
-        for k, name in ((0, "wo start"), (1, "wo passed"), (2, "wo end")):
+        for k, name in ((0, "wo start"), (1, "wo passed"), (3, "wo staged"), (2, "wo end")):
             v = np.array([us(t[i, k]) for i in wo])
             print(f"{name:15s}  min {v.min():6.2f} med {np.median(v):6.2f} max {v.max():6.2f} us")
     m.close()

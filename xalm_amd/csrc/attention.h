@@ -49,6 +49,11 @@ __device__ __host__ __forceinline__ int attn_split_len(const int kv_len, const i
 }
 // one round of K/V rows per block: the split floor of a THREADS-thread block
 __device__ __host__ constexpr int attn_min_t(const int hd, const int threads) { return ATTN_PREF * threads / (hd / 8); }
+// the fused launch's floor: half a round (each split block pulls half the bytes: a block's
+// K/V fetch is bound by its CU's ~60 GB/s, so more, smaller splits shorten the chain)
+__device__ __host__ constexpr int attn_min_t_partials(const int hd, const int threads) {
+    return attn_min_t(hd, threads) / 2;
+}
 
 __device__ __forceinline__ float ld_sc1(const float* p) {
     return __builtin_bit_cast(float, __hip_atomic_load((const uint32_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
@@ -75,7 +80,7 @@ __device__ __forceinline__ void attn_block(const AttnArgs& a, const int g, const
     int* flag = (int*)(ml + 2 * QPK);
 
     const int kv_len = a.sp->kv_len;
-    constexpr int MIN_T = PARTIALS ? attn_min_t(HD, THREADS) : ATTN_MIN_T;
+    constexpr int MIN_T = PARTIALS ? attn_min_t_partials(HD, THREADS) : ATTN_MIN_T;
     const int T = attn_split_len(kv_len, a.nsplit, MIN_T);
     const int t0 = s * T;
     if (t0 >= kv_len) return;
@@ -194,16 +199,44 @@ __device__ __forceinline__ void attn_block(const AttnArgs& a, const int g, const
     }
     ATTN_STAMP(7);
     // reduce over the row slots of this wave (lanes sharing `sub`), then over waves (fixed order)
-#pragma unroll
-    for (int h = 0; h < QPK; h++)
-#pragma unroll
-        for (int i = 0; i < 8; i++)
-            acc[h][i] = strided_reduce<LPR>(acc[h][i]);
-    if (lane < LPR) {
+    if constexpr (LPR <= 16 && QPK * 8 >= 4) {
+        // slots inside a 16-lane row first (DPP), then a reduce-scatter over the 4 rows: each
+        // row ends with a quarter of the QPK*8 values, written by its first LPR lanes
+        constexpr int N = QPK * 8;
+        float v[N];
 #pragma unroll
         for (int h = 0; h < QPK; h++)
 #pragma unroll
-            for (int i = 0; i < 8; i++) red[wid * NO + h * HD + sub * 8 + i] = acc[h][i];
+            for (int i = 0; i < 8; i++) {
+                float x = acc[h][i];
+                if (LPR <= 1) x += dpp<DPP_ROW_ROR + 1>(x);
+                if (LPR <= 2) x += dpp<DPP_ROW_ROR + 2>(x);
+                if (LPR <= 4) x += dpp<DPP_ROW_ROR + 4>(x);
+                if (LPR <= 8) x += dpp<DPP_ROW_ROR + 8>(x);
+                v[h * 8 + i] = x;
+            }
+        rows_reduce_scatter<N>(v);
+        const int r = lane >> 4;
+        const int vb = (r & 1) * (N / 2) + (r >> 1) * (N / 4);
+        if ((lane & 15) < LPR) {
+#pragma unroll
+            for (int k = 0; k < N / 4; k++) {
+                const int vi = vb + k;
+                red[wid * NO + (vi >> 3) * HD + sub * 8 + (vi & 7)] = v[k];
+            }
+        }
+    } else {
+#pragma unroll
+        for (int h = 0; h < QPK; h++)
+#pragma unroll
+            for (int i = 0; i < 8; i++)
+                acc[h][i] = strided_reduce<LPR>(acc[h][i]);
+        if (lane < LPR) {
+#pragma unroll
+            for (int h = 0; h < QPK; h++)
+#pragma unroll
+                for (int i = 0; i < 8; i++) red[wid * NO + h * HD + sub * 8 + i] = acc[h][i];
+        }
     }
     __syncthreads();
     auto block_sum = [&](const int idx) {

@@ -40,21 +40,31 @@ __host__ __device__ constexpr size_t aw_image_bytes(const int n) {
 }
 
 // x image of the Wo rows = the merged attention output.  wts: LDS [n_heads][n_active] weights,
-// [n_heads] denominators, then the (m, l) pairs [n_active][n_heads][2].
+// [n_heads] denominators, then the (m, l) pairs [n_active][n_heads][2].  The partial-o loads
+// of a thread's first float4 are issued together with the (m, l) loads (one round trip).
 template <int E, int HD>
 __device__ __forceinline__ void aw_stage_merged(const AttnArgs& aa, const int n, const int n_active, float4* xs4,
                                                 float* wts) {
+    constexpr int MAXS = 4;  // prefetched partials per thread (registers beside the Wo rows)
     const int tid = threadIdx.x;
     const int nh = aa.n_heads;
-    // (m, l) of every split and head: one batched pass of sc1 loads into LDS ...
+    const int n4 = n >> 2;
+    const size_t stride = (size_t)nh * HD;  // floats per split in part_o
+    const bool pre = n_active <= MAXS && tid < n4;
+    u32x4 ov[MAXS];
+    if (pre) {
+#pragma unroll
+        for (int j = 0; j < MAXS; j++)
+            if (j < n_active) ov[j] = ld_sc1_x4(aa.part_o, (uint32_t)((j * stride + 4 * (size_t)tid) * 4));
+    }
     float* ml = wts + nh * (n_active + 1);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)aa.part_ml, 0, 0x7fffffff, 0x00020000);
     for (int i = tid; i < n_active * nh; i += AW_THREADS) {
-        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)aa.part_ml, 0, 0x7fffffff, 0x00020000);
         ml[2 * i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, i * 8, 0, 16));  // sc1
         ml[2 * i + 1] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, i * 8 + 4, 0, 16));
     }
     __syncthreads();
-    // ... then per head: weights e^{m_s - M} and the denominator sum_s e^{m_s - M} l_s
+    // per head: weights e^{m_s - M} and the denominator sum_s e^{m_s - M} l_s
     for (int h = tid; h < nh; h += AW_THREADS) {
         float M = -FLT_MAX;
         for (int j = 0; j < n_active; j++) M = fmaxf(M, ml[2 * (j * nh + h)]);
@@ -67,17 +77,23 @@ __device__ __forceinline__ void aw_stage_merged(const AttnArgs& aa, const int n,
         wts[nh * n_active + h] = den;
     }
     __syncthreads();
-    const size_t stride = (size_t)nh * HD;  // floats per split in part_o
-    for (int i = tid; i < (n >> 2); i += AW_THREADS) {
+    for (int i = tid; i < n4; i += AW_THREADS) {
         const int h = (4 * i) / HD;
         const float* w = wts + h * n_active;
         float4 num = make_float4(0.f, 0.f, 0.f, 0.f);
-        for (int j = 0; j < n_active; j++) {
-            const u32x4 u = ld_sc1_x4(aa.part_o, (uint32_t)((j * stride + 4 * (size_t)i) * 4));
-            num.x = fmaf(w[j], bits_f32(u.x), num.x);
-            num.y = fmaf(w[j], bits_f32(u.y), num.y);
-            num.z = fmaf(w[j], bits_f32(u.z), num.z);
-            num.w = fmaf(w[j], bits_f32(u.w), num.w);
+        auto add = [&](const float wj, const u32x4 u) {
+            num.x = fmaf(wj, bits_f32(u.x), num.x);
+            num.y = fmaf(wj, bits_f32(u.y), num.y);
+            num.z = fmaf(wj, bits_f32(u.z), num.z);
+            num.w = fmaf(wj, bits_f32(u.w), num.w);
+        };
+        if (pre && i == tid) {
+#pragma unroll
+            for (int j = 0; j < MAXS; j++)
+                if (j < n_active) add(w[j], ov[j]);
+        } else {
+            for (int j = 0; j < n_active; j++)
+                add(w[j], ld_sc1_x4(aa.part_o, (uint32_t)((j * stride + 4 * (size_t)i) * 4)));
         }
         const float den = wts[nh * n_active + h];
         const float4 v = make_float4(num.x / den, num.y / den, num.z / den, num.w / den);
@@ -115,7 +131,7 @@ __global__ __launch_bounds__(AW_THREADS) void attn_wo_kernel(const AttnArgs aa, 
     const int g = (b - n_att) * S::WAVES + wid;
     auto wait_heads = [&]() {
         const int kv_len = aa.sp->kv_len;
-        const int T = attn_split_len(kv_len, aa.nsplit, attn_min_t(HD, AW_THREADS));
+        const int T = attn_split_len(kv_len, aa.nsplit, attn_min_t_partials(HD, AW_THREADS));
         const int n_active = (kv_len + T - 1) / T;
         if (threadIdx.x == 0) {
             const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
@@ -132,15 +148,27 @@ __global__ __launch_bounds__(AW_THREADS) void attn_wo_kernel(const AttnArgs aa, 
         if (trace && threadIdx.x == 0) trace[8 * b + 1] = __builtin_amdgcn_s_memrealtime();
         aw_stage_merged<E, HD>(aa, ga.n, n_active, xs4, (float*)(smem + LDS_HEAD_BYTES + aw_image_bytes<E>(ga.n)));
         __syncthreads();
+        if (trace && threadIdx.x == 0) trace[8 * b + 3] = __builtin_amdgcn_s_memrealtime();
     };
     const int n_groups = gemv_groups<S>(ga);
     if (ga.n == S::U * 64 * E && n_groups <= nb * S::WAVES) {
         // every wave owns at most one group and its whole rows fit the U chunks: request them,
         // then wait; nothing but the dot products is left after the hand-off
+        // wave 0 polls, so it requests its rows only after the hand-off: a poll's sc1 load
+        // completes in order behind the polling wave's own outstanding loads (vmcnt)
         u32x4 w[S::U][S::ROWS];
-        if (g < n_groups && !(ga.act & 256)) gemv_prefetch<S>(ga, g, lane, w);
+        float xres[S::ROWS];
+        auto fetch = [&]() {
+            gemv_prefetch<S>(ga, g, lane, w);
+            if (lane == 0) {
+#pragma unroll
+                for (int r = 0; r < S::ROWS; r++) xres[r] = g * S::ROWS + r < ga.rows ? ga.out[g * S::ROWS + r] : 0.f;
+            }
+        };
+        const bool early = wid != 0 && !(ga.act & 256);
+        if (g < n_groups && early) fetch();
         wait_heads();
-        if (g < n_groups && (ga.act & 256)) gemv_prefetch<S>(ga, g, lane, w);
+        if (g < n_groups && !early) fetch();
         if (g < n_groups) {
             float acc[S::ROWS];
 #pragma unroll
@@ -148,7 +176,11 @@ __global__ __launch_bounds__(AW_THREADS) void attn_wo_kernel(const AttnArgs aa, 
             gemv_compute<DT, S::ROWS, S::U>(w, xs4, 0, lane, acc);
 #pragma unroll
             for (int r = 0; r < S::ROWS; r++) acc[r] = wave_sum(acc[r]);
-            if (lane == 0) gemv_epilogue<EPI_RESID, S::ROWS>(ga, g * S::ROWS, acc);
+            if (lane == 0) {
+#pragma unroll
+                for (int r = 0; r < S::ROWS; r++)  // x += Wo . attn (src/infer.cpp:449-452)
+                    if (g * S::ROWS + r < ga.rows) ga.out[g * S::ROWS + r] = xres[r] + acc[r];
+            }
         }
     } else {
         using G = GemvShape<AW_THREADS, S::ROWS, 4, true, 4, false>;

@@ -178,6 +178,27 @@ __device__ __forceinline__ float strided_reduce(float v) {
     v = halves<Op>(v);
     return v;
 }
+// Reduce-scatter of N per-lane values over the four 16-lane rows of a wave: on return v[0, N/4)
+// of every lane of row r holds the 4-row sums of values [(r & 1) * N/2 + (r >> 1) * N/4, + N/4)
+// (N/2 + N/4 swaps instead of 2 N for a full all-reduce of every value).
+template <int N>
+__device__ __forceinline__ void rows_reduce_scatter(float (&v)[N]) {
+    static_assert(N % 4 == 0, "N must be a multiple of 4");
+    // each swap carries its own s_nop 1: the operands may be fresh VALU copies (T21 hazard)
+#pragma unroll
+    for (int k = 0; k < N / 2; k++) {
+        float x = v[k], y = v[N / 2 + k];
+        asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(x), "+v"(y));
+        v[k] = x + y;
+    }
+#pragma unroll
+    for (int k = 0; k < N / 4; k++) {
+        float x = v[k], y = v[N / 4 + k];
+        asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(x), "+v"(y));
+        v[k] = x + y;
+    }
+}
+
 __device__ __forceinline__ float wave_sum(float v) { return group_reduce<64, OpSum>(v); }
 __device__ __forceinline__ float wave_max(float v) { return group_reduce<64, OpMax>(v); }
 

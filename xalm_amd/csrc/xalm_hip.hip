@@ -598,7 +598,7 @@ int xh_create(const xh_config* cfg, int device_ordinal, xh_ctx** out) {
     ctx->qpk = qpk;
     ctx->nsplit = attn_nsplit(c.n_kv_heads, c.max_seq_len);
     ctx->t_max = attn_split_len(c.max_seq_len, ctx->nsplit);
-    ctx->t_max_aw = attn_split_len(c.max_seq_len, ctx->nsplit, attn_min_t(c.head_dim, AW_THREADS));
+    ctx->t_max_aw = attn_split_len(c.max_seq_len, ctx->nsplit, attn_min_t_partials(c.head_dim, AW_THREADS));
     int rc = 0;
 #define CREATE_TRY(expr) do { rc = (expr); if (rc) { g_create_error = ctx->err; xh_destroy(ctx); return rc; } } while (0)
     if (hipSetDevice(device_ordinal) != hipSuccess) { delete ctx; return set_err(nullptr, XH_E_HIP, "hipSetDevice failed"); }
