@@ -92,6 +92,21 @@ def prompt_tokens(vocab, n=32, seed=7):
     return out
 
 
+def pmc_traffic(kernel_prefix):
+    """Read bytes per dispatch of a kernel from the newest committed PMC summary
+    (profiles/*_pmc.json, written by tools/pmc.sh: FETCH_SIZE x2 + WRITE_SIZE, separate
+    rocprofv3 passes).  None when no summary covers the kernel."""
+    import glob
+    files = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "*_pmc.json")))
+    for f in reversed(files):
+        with open(f) as fh:
+            ks = json.load(fh)["kernels"]
+        for name, v in ks.items():
+            if name.startswith(kernel_prefix) and v.get("read_bytes_avg") is not None:
+                return int(v["read_bytes_avg"] + (v.get("write_bytes_avg") or 0)), os.path.basename(f)
+    return None, None
+
+
 def sync_all(dist, torch_mod):
     if torch_mod is not None and torch_mod.cuda.is_available():
         torch_mod.cuda.synchronize()
@@ -232,8 +247,10 @@ def main():
                     "kernel": "persistent_decode_kernel (all phases of all timed tokens, one launch)",
                     "bytes_per_launch": step_bytes, "avg_launch_us": round(launch_us, 1)}
     else:
+        traffic, src = pmc_traffic("void xalm::gemv_kernel<%d, 1, 3," % w["wdt"])
         roofline = {"bound": "hbm", "achieved": round(k_gbps, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                    "frac": round(k_gbps / HBM_PEAK_GBPS, 4), "traffic": None,
+                    "frac": round(k_gbps / HBM_PEAK_GBPS, 4), "traffic": traffic,
+                    "traffic_source": src,
                     "kernel": "gemv_kernel<PRO_RMSNORM,EPI_GLU> (fused W1/W3 + rmsnorm + silu*up), layer 0",
                     "bytes_per_launch": k_bytes, "avg_launch_us": round(k_us, 2)}
     value = world * args.steps / elapsed
