@@ -186,7 +186,7 @@ __global__ __launch_bounds__(AW_THREADS) void attn_wo_kernel(const AttnArgs aa, 
         using G = GemvShape<AW_THREADS, S::ROWS, 4, true, 4, false>;
         wait_heads();
         u32x4 none[G::U][G::ROWS];
-        gemv_rows<DT, EPI_RESID, G>(ga, g, nb * S::WAVES, lane, xs4, none, false);
+        gemv_rows<DT, EPI_RESID, G, false>(ga, g, nb * S::WAVES, lane, xs4, none);
     }
     __syncthreads();
     if (trace && threadIdx.x == 0) trace[8 * b + 2] = __builtin_amdgcn_s_memrealtime();

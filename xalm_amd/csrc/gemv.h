@@ -27,7 +27,7 @@ enum { EPI_STORE = 0, EPI_RESID = 1, EPI_QKV = 2, EPI_GLU = 3 };
 constexpr int LDS_HEAD_BYTES = 64;  // block-reduction scratch in front of the x image
 
 // Launch shape of one gemv instance.
-template <int THREADS_, int ROWS_, int U_, bool NT_ = true, int MINW_ = 4, bool PF_ = true>
+template <int THREADS_, int ROWS_, int U_, bool NT_ = true, int MINW_ = 4, bool PF_ = true, int XN_ = 0>
 struct GemvShape {
     static constexpr int THREADS = THREADS_;   // workgroup size
     static constexpr int WAVES = THREADS_ / 64;
@@ -35,7 +35,8 @@ struct GemvShape {
     static constexpr int U = U_;               // 16-B chunks per row in flight
     static constexpr bool NT = NT_;            // non-temporal weight loads
     static constexpr int MINW = MINW_;         // __launch_bounds__ min waves per SIMD
-    static constexpr bool PF = PF_;            // first chunk requested before the x prologue
+    static constexpr bool PF = PF_;            // first U chunks requested inside the x prologue
+    static constexpr int XN = XN_;             // PF: float4 of x (and norm) per thread held in registers
 };
 
 struct GemvArgs {
@@ -61,7 +62,19 @@ struct GemvArgs {
     float qkv_clip;
     int act;
     const StepParams* sp;
+    unsigned long long* trace;  // debug (null = off): per workgroup [4] start, x staged, rows done
 };
+
+// agent-scope relaxed (sc1: L1-bypassing, write-through) accesses for data handed between
+// kernels that run concurrently (chain.h)
+__device__ __forceinline__ uint32_t ld_sc1_u32(const void* p) {
+    return __hip_atomic_load((const uint32_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_sc1_u32(void* p, const uint32_t v) {
+    __hip_atomic_store((uint32_t*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_sc1_f(const float* p) { return __builtin_bit_cast(float, ld_sc1_u32(p)); }
+__device__ __forceinline__ void st_sc1_f(float* p, const float v) { st_sc1_u32(p, __builtin_bit_cast(uint32_t, v)); }
 
 __device__ __forceinline__ float clipf(const float x, const float v) { return x < -v ? -v : (x > v ? v : x); }
 
@@ -114,6 +127,17 @@ __device__ __forceinline__ float4 load_norm4(const void* w, const int dtype, con
     return ((const float4*)w)[i4];
 }
 
+// Branch-free form of load_norm4 for the PF prologue: one 16-byte buffer load at the
+// dtype's stride (bounds-checked by the descriptor: the bytes past the vector read as 0), then
+// selects.  norm dtype is F32 or BF16.
+__device__ __forceinline__ float4 load_norm4_nb(const void* w, const int dtype, const int n, const int i4) {
+    const bool bf = dtype == XH_BF16;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)w, 0, n * (bf ? 2 : 4), 0x00020000);
+    const u32x4 u = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, i4 * (bf ? 8 : 16), 0, 0));
+    return make_float4(bf ? bits_f32(u.x << 16) : bits_f32(u.x), bf ? bits_f32(u.x & 0xffff0000u) : bits_f32(u.y),
+                       bf ? bits_f32(u.y << 16) : bits_f32(u.z), bf ? bits_f32(u.y & 0xffff0000u) : bits_f32(u.w));
+}
+
 // x (optionally rms-normalised and weighted) -> LDS image xs4, permuted so that lane l at
 // chunk `it` finds the E/4 float4 it multiplies at xs4[(it*E/4 + q)*64 + l].
 // SC1: x was published inside the running launch (write-through): read it with sc1 loads.
@@ -163,19 +187,26 @@ __device__ __forceinline__ void rotate_sinks(const GemvArgs& a, const int kv_sin
     }
 }
 
-template <int EPI, int ROWS>
+// SC1: activations another in-flight kernel reads are stored write-through, and the residual
+// it may have written is read with sc1 loads (chain.h); otherwise plain accesses.
+template <bool SC1>
+__device__ __forceinline__ void epi_st(float* p, const float v) {
+    if (SC1) st_sc1_f(p, v);
+    else *p = v;
+}
+template <int EPI, int ROWS, bool SC1 = false>
 __device__ __forceinline__ void gemv_epilogue(const GemvArgs& a, const int row0, const float* acc) {
     if (EPI == EPI_STORE) {
 #pragma unroll
         for (int r = 0; r < ROWS; r++)
-            if (row0 + r < a.rows) a.out[row0 + r] = acc[r];
+            if (row0 + r < a.rows) epi_st<SC1>(a.out + row0 + r, acc[r]);
     } else if (EPI == EPI_RESID) {
 #pragma unroll
         for (int r = 0; r < ROWS; r++)
-            if (row0 + r < a.rows) a.out[row0 + r] += acc[r];
+            if (row0 + r < a.rows) epi_st<SC1>(a.out + row0 + r, (SC1 ? ld_sc1_f(a.out + row0 + r) : a.out[row0 + r]) + acc[r]);
     } else if (EPI == EPI_GLU) {
 #pragma unroll
-        for (int p = 0; p < ROWS; p += 2) a.out[(row0 + p) >> 1] = act_fn(a.act, acc[p]) * acc[p + 1];
+        for (int p = 0; p < ROWS; p += 2) epi_st<SC1>(a.out + ((row0 + p) >> 1), act_fn(a.act, acc[p]) * acc[p + 1]);
     } else {  // EPI_QKV
         const int pos = a.sp->pos;
         const int kv_pos = a.sp->kv_pos;
@@ -185,19 +216,17 @@ __device__ __forceinline__ void gemv_epilogue(const GemvArgs& a, const int row0,
             float v0 = clipf(acc[p], a.qkv_clip), v1 = clipf(acc[p + 1], a.qkv_clip);
             if (row < a.q_dim) {
                 rope_pair(v0, v1, row, a.head_dim, pos, a.rope_freq);
-                a.q[row] = v0;
-                a.q[row + 1] = v1;
-            } else if (row < a.q_dim + a.kv_dim) {
-                const int kr = row - a.q_dim;
-                rope_pair(v0, v1, kr, a.head_dim, pos, a.rope_freq);
-                uint16_t* dst = a.kcache + (size_t)kv_pos * a.kv_dim + kr;
-                dst[0] = f32_to_f16_bits(v0);
-                dst[1] = f32_to_f16_bits(v1);
+                epi_st<SC1>(a.q + row, v0);
+                epi_st<SC1>(a.q + row + 1, v1);
             } else {
-                const int vr = row - a.q_dim - a.kv_dim;
-                uint16_t* dst = a.vcache + (size_t)kv_pos * a.kv_dim + vr;
-                dst[0] = f32_to_f16_bits(v0);
-                dst[1] = f32_to_f16_bits(v1);
+                const bool isk = row < a.q_dim + a.kv_dim;
+                const int kr = isk ? row - a.q_dim : row - a.q_dim - a.kv_dim;
+                if (isk) rope_pair(v0, v1, kr, a.head_dim, pos, a.rope_freq);
+                uint16_t* dst = (isk ? a.kcache : a.vcache) + (size_t)kv_pos * a.kv_dim + kr;
+                // the pair as one 4-byte store (kr is even)
+                const uint32_t pk = (uint32_t)f32_to_f16_bits(v0) | ((uint32_t)f32_to_f16_bits(v1) << 16);
+                if (SC1) st_sc1_u32(dst, pk);
+                else *(uint32_t*)dst = pk;
             }
         }
     }
@@ -274,63 +303,152 @@ __device__ __forceinline__ void gemv_prefetch(const GemvArgs& a, const int g, co
     gemv_load<S::ROWS, S::U, S::NT>(pre, wrow, rs, 0);
 }
 
-// Groups g, g + total_waves, ... of this wave against the staged x image; the first group
-// starts from `pre` when `first` (its chunks [0, U) already requested).
-template <int DT, int EPI, class S>
-__device__ __forceinline__ void gemv_rows(const GemvArgs& a, int g, const int total_waves, const int lane,
-                                          const float4* xs4, const u32x4 (&pre)[S::U][S::ROWS], bool first) {
+// Chunks [it, n) of group g into acc, then the wave reduction and the epilogue.
+template <int DT, int EPI, class S, bool SC1 = false>
+__device__ __forceinline__ void gemv_group(const GemvArgs& a, const int g, const int lane, const float4* xs4, float* acc,
+                                           int it) {
     constexpr int ROWS = S::ROWS, U = S::U;
     constexpr int E = WDec<DT>::E;
     const int n = a.n;
     const int n_full = n / (64 * E);
     const int n_it = (n + 64 * E - 1) / (64 * E);
+    size_t rstride;
+    const char* wrow = gemv_row_ptr<ROWS>(a, g, lane, rstride);
+    for (; it + U <= n_full; it += U) gemv_chunk<DT, ROWS, U, S::NT>(wrow, rstride, xs4, it, lane, acc);
+    if (U > 2)
+        for (; it + 2 <= n_full; it += 2) gemv_chunk<DT, ROWS, 2, S::NT>(wrow, rstride, xs4, it, lane, acc);
+    for (; it < n_full; it++) gemv_chunk<DT, ROWS, 1, S::NT>(wrow, rstride, xs4, it, lane, acc);
+    if (it < n_it && (it * 64 + lane) * E < n) gemv_chunk<DT, ROWS, 1, S::NT>(wrow, rstride, xs4, it, lane, acc);
+#pragma unroll
+    for (int r = 0; r < ROWS; r++) acc[r] = wave_sum(acc[r]);
+    if (lane == 0) gemv_epilogue<EPI, ROWS, SC1>(a, g * ROWS, acc);
+}
+
+// Groups g, g + total_waves, ... of this wave against the staged x image.  FIRST: the first
+// group's chunks [0, U) are already in `pre` (the caller checked g < groups and n_full >= U);
+// that group is peeled so `pre` is dead in the loop.
+template <int DT, int EPI, class S, bool FIRST, bool SC1 = false>
+__device__ __forceinline__ void gemv_rows(const GemvArgs& a, int g, const int total_waves, const int lane,
+                                          const float4* xs4, const u32x4 (&pre)[S::U][S::ROWS]) {
     const int n_groups = gemv_groups<S>(a);
+    if (FIRST) {
+        float acc[S::ROWS];
+#pragma unroll
+        for (int r = 0; r < S::ROWS; r++) acc[r] = 0.f;
+        gemv_compute<DT, S::ROWS, S::U>(pre, xs4, 0, lane, acc);
+        gemv_group<DT, EPI, S, SC1>(a, g, lane, xs4, acc, S::U);
+        g += total_waves;
+    }
     for (; g < n_groups; g += total_waves) {
-        size_t rstride;
-        const char* wrow = gemv_row_ptr<ROWS>(a, g, lane, rstride);
-        float acc[ROWS];
+        float acc[S::ROWS];
 #pragma unroll
-        for (int r = 0; r < ROWS; r++) acc[r] = 0.f;
-        int it = 0;
-        if (first) {
-            gemv_compute<DT, ROWS, U>(pre, xs4, 0, lane, acc);
-            it = U;
-            first = false;
+        for (int r = 0; r < S::ROWS; r++) acc[r] = 0.f;
+        gemv_group<DT, EPI, S, SC1>(a, g, lane, xs4, acc, 0);
+    }
+}
+
+// PF staging, part 1: this thread's x float4s (and norm weights) into registers.  Issued
+// BEFORE the weight prefetch, so waiting for them (vmcnt counts in issue order) leaves the
+// weight chunks in flight.
+template <int PRO, class S>
+__device__ __forceinline__ void stage_x_issue(const GemvArgs& a, float4 (&xv)[S::XN], float4 (&nw)[S::XN]) {
+    const int n4 = a.n >> 2;
+    const float4* x4 = (const float4*)a.x;
+    // clamped indices, no branches: every load of the prologue sits in one basic block, so the
+    // waits for x count only the x loads (threads past n4 reload the last float4; unused)
+#pragma unroll
+    for (int j = 0; j < S::XN; j++) {
+        const int i = min((int)threadIdx.x + j * S::THREADS, n4 - 1);
+        xv[j] = x4[i];
+        if (PRO == PRO_RMSNORM) nw[j] = load_norm4_nb(a.norm_w, a.norm_dtype, a.n, i);
+    }
+}
+// part 2: rms scale (same per-thread order, shuffle tree and wave order as block_rms_scale, so
+// the same value) and the permuted LDS image.  Branch-free like part 1 (a branch would let the
+// compiler sink a load to its use and wait for the weights too): clamped duplicates are
+// masked out of the sum and store the same value to the same slot.
+template <int E, int PRO, class S>
+__device__ __forceinline__ void stage_x_finish(const GemvArgs& a, const float4 (&xv)[S::XN], const float4 (&nw)[S::XN],
+                                               float4* xs4, float* red) {
+    const int n4 = a.n >> 2;
+    float scale = 1.f;
+    if (PRO == PRO_RMSNORM) {
+        float ss = 0.f;
+#pragma unroll
+        for (int j = 0; j < S::XN; j++) {
+            const float4 v = xv[j];
+            const float d = v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+            ss += ((int)threadIdx.x + j * S::THREADS < n4) ? d : 0.f;
         }
-        for (; it + U <= n_full; it += U) gemv_chunk<DT, ROWS, U, S::NT>(wrow, rstride, xs4, it, lane, acc);
-        if (U > 2)
-            for (; it + 2 <= n_full; it += 2) gemv_chunk<DT, ROWS, 2, S::NT>(wrow, rstride, xs4, it, lane, acc);
-        for (; it < n_full; it++) gemv_chunk<DT, ROWS, 1, S::NT>(wrow, rstride, xs4, it, lane, acc);
-        if (it < n_it && (it * 64 + lane) * E < n) gemv_chunk<DT, ROWS, 1, S::NT>(wrow, rstride, xs4, it, lane, acc);
+        ss = wave_sum(ss);
+        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
+        __syncthreads();
+        float tot = 0.f;
 #pragma unroll
-        for (int r = 0; r < ROWS; r++) acc[r] = wave_sum(acc[r]);
-        if (lane == 0) gemv_epilogue<EPI, ROWS>(a, g * ROWS, acc);
+        for (int w = 0; w < S::WAVES; w++) tot += red[w];
+        scale = 1.0f / sqrtf(tot / (float)a.n + a.eps);
+    }
+#pragma unroll
+    for (int j = 0; j < S::XN; j++) {
+        const int i = min((int)threadIdx.x + j * S::THREADS, n4 - 1);
+        float4 v = xv[j];
+        if (PRO == PRO_RMSNORM) {
+            v.x = v.x * scale * nw[j].x;  // x[i] * scale * weight[i], src/infer.cpp:234
+            v.y = v.y * scale * nw[j].y;
+            v.z = v.z * scale * nw[j].z;
+            v.w = v.w * scale * nw[j].w;
+        }
+        const int c = i << 2;
+        const int it = c / (64 * E);
+        const int rem = c - it * 64 * E;
+        const int l = rem / E;
+        const int qd = (rem - l * E) >> 2;
+        xs4[(it * (E / 4) + qd) * 64 + l] = v;
     }
 }
 
 // Grid: every wave owns the same number of ROWS-row groups (g = wave, wave + W, ...), so no
-// wave is left with a partial last round.  The first U weight chunks of the first group are
-// requested before the x image is staged, so HBM latency overlaps the prologue.
+// wave is left with a partial last round.  PF shapes (host-checked: n <= 4 * XN * THREADS and
+// n >= 64 * E * U):
+// x (and the norm weights) are requested first, then the first U weight chunks of the wave's
+// first group, so the HBM round trip of the weights overlaps the x prologue.
 template <int DT, int PRO, int EPI, class S>
 __global__ __launch_bounds__(S::THREADS, S::MINW) void gemv_kernel(const GemvArgs a) {
-    constexpr int ROWS = S::ROWS, U = S::U;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     float* red = (float*)smem;
     float4* xs4 = (float4*)(smem + LDS_HEAD_BYTES);
     constexpr int E = WDec<DT>::E;
     const int lane = threadIdx.x & 63;
     const int wid = threadIdx.x >> 6;
-
     const int g = blockIdx.x * S::WAVES + wid;
+    if (a.trace && threadIdx.x == 0) a.trace[4 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
 
-    const bool prefetched = S::PF && g < gemv_groups<S>(a) && a.n / (64 * E) >= U;
-    u32x4 pre[U][ROWS];
-    if (prefetched) gemv_prefetch<S>(a, g, lane, pre);
-
-    stage_x<E, PRO, S::THREADS>(a, xs4, red);
-    if (EPI == EPI_QKV && blockIdx.x == 0) rotate_sinks<S::THREADS>(a, a.sp->kv_sink);
-    __syncthreads();
-    gemv_rows<DT, EPI, S>(a, g, gridDim.x * S::WAVES, lane, xs4, pre, prefetched);
+    if constexpr (S::PF) {
+        float4 xv[S::XN], nw[S::XN];
+        stage_x_issue<PRO, S>(a, xv, nw);
+        // unconditional (a wave past the last group re-reads that group's chunks, unused)
+        const int n_groups = gemv_groups<S>(a);
+        const bool prefetched = g < n_groups;
+        u32x4 pre[S::U][S::ROWS];
+        gemv_prefetch<S>(a, min(g, n_groups - 1), lane, pre);
+        stage_x_finish<E, PRO, S>(a, xv, nw, xs4, red);
+        if (EPI == EPI_QKV && blockIdx.x == 0) rotate_sinks<S::THREADS>(a, a.sp->kv_sink);
+        __syncthreads();
+        if (a.trace && threadIdx.x == 0) a.trace[4 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+        if (prefetched) gemv_rows<DT, EPI, S, true>(a, g, gridDim.x * S::WAVES, lane, xs4, pre);
+        else gemv_rows<DT, EPI, S, false>(a, g, gridDim.x * S::WAVES, lane, xs4, pre);
+    } else {
+        stage_x<E, PRO, S::THREADS>(a, xs4, red);
+        if (EPI == EPI_QKV && blockIdx.x == 0) rotate_sinks<S::THREADS>(a, a.sp->kv_sink);
+        __syncthreads();
+        if (a.trace && threadIdx.x == 0) a.trace[4 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+        u32x4 none[S::U][S::ROWS];
+        gemv_rows<DT, EPI, S, false>(a, g, gridDim.x * S::WAVES, lane, xs4, none);
+    }
+    if (a.trace) {
+        __syncthreads();
+        if (threadIdx.x == 0) a.trace[4 * blockIdx.x + 2] = __builtin_amdgcn_s_memrealtime();
+    }
 }
 
 // LDS bytes and grid of one launch

@@ -85,17 +85,6 @@ struct PkArgs {
 constexpr int PK_TRACE_WG = 3;
 __host__ __device__ constexpr int pk_trace_len(int n_layers) { return (n_layers + 1) * PK_PHASES * 2 + 2; }
 
-// ---- sc1 (write-through, L1-bypassing) accesses -----------------------------------------
-__device__ __forceinline__ void st_sc1_u32(void* p, const uint32_t v) {
-    __hip_atomic_store((uint32_t*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint32_t ld_sc1_u32(const void* p) {
-    return __hip_atomic_load((const uint32_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ float ld_sc1_f(const float* p) { return __builtin_bit_cast(float, ld_sc1_u32(p)); }
-__device__ __forceinline__ void st_sc1_f(float* p, float v) { st_sc1_u32(p, __builtin_bit_cast(uint32_t, v)); }
-
-
 // threadIdx.x behind an empty asm: thread-derived addresses are recomputed where they are
 // used instead of being hoisted out of the token/layer loops and kept live (they spilled)
 __device__ __forceinline__ int pk_tid() {

@@ -136,11 +136,15 @@ int set_err(xh_ctx* ctx, int code, const char* fmt, ...) {
 // ---------------------------------------------------------------------------------------
 // gemv launch dispatch
 // ---------------------------------------------------------------------------------------
-// Shapes, chosen with tools/gemv_bench.hip on MI355X (profiles/r01_gemv_bench.txt): 512-thread
-// blocks (8 waves share one x image), 2 rows x 4 chunks in flight per wave, non-temporal
-// weight loads, 16 waves per CU, no register prefetch ahead of the prologue (it spills).
+// Shapes, chosen with tools/gemv_bench.hip and tools/chain_bench.hip on MI355X
+// (profiles/r01_gemv_bench.txt, profiles/r01_chain_bench.txt): 512-thread blocks (8 waves share
+// one x image), 2 rows x 4 chunks in flight per wave, non-temporal weight loads, 16 waves per
+// CU.  PF shapes hold x in registers (XN float4 per thread) and request the first weight chunks
+// inside the prologue (-5.7 % per decode layer); the plain shape covers every other n.
 using ShapeShort = GemvShape<512, ROWS, UNROLL, true, 4, false>;
 using ShapeLong = GemvShape<512, ROWS, UNROLL, true, 4, false>;
+using ShapePF2 = GemvShape<512, ROWS, UNROLL, true, 4, true, 2>;  // n <= 4096
+using ShapePF8 = GemvShape<512, ROWS, UNROLL, true, 4, true, 8>;  // n <= 16384 (W2 / Wo inputs)
 
 template <int DT, int PRO, int EPI, class S>
 void launch_gemv_s(const GemvArgs& a, hipStream_t s, int max_waves) {
@@ -159,8 +163,18 @@ void launch_gemv_s(const GemvArgs& a, hipStream_t s, int max_waves) {
 
 template <int DT, int PRO, int EPI>
 void launch_gemv_t(const GemvArgs& a, hipStream_t s, int max_waves) {
-    if (gemv_smem_bytes<DT, ShapeShort>(a.n) <= 40 * 1024) launch_gemv_s<DT, PRO, EPI, ShapeShort>(a, s, max_waves);
-    else launch_gemv_s<DT, PRO, EPI, ShapeLong>(a, s, max_waves);
+    constexpr int E = WDec<DT>::E;
+    // PF needs whole first chunks (n >= 64 E U) and x in XN float4 per thread
+    const bool pf = a.n % 4 == 0 && a.n >= 64 * E * UNROLL;
+    if (pf && a.n / 4 <= 2 * 512) launch_gemv_s<DT, PRO, EPI, ShapePF2>(a, s, max_waves);
+    else if constexpr (PRO == PRO_PLAIN) {
+        if (pf && a.n / 4 <= 8 * 512) launch_gemv_s<DT, PRO, EPI, ShapePF8>(a, s, max_waves);
+        else launch_gemv_s<DT, PRO, EPI, ShapeLong>(a, s, max_waves);
+    } else if (gemv_smem_bytes<DT, ShapeShort>(a.n) <= 40 * 1024) {
+        launch_gemv_s<DT, PRO, EPI, ShapeShort>(a, s, max_waves);
+    } else {
+        launch_gemv_s<DT, PRO, EPI, ShapeLong>(a, s, max_waves);
+    }
 }
 
 template <int PRO, int EPI>
