@@ -159,8 +159,8 @@ def main():
     ap.add_argument("--kernel-iters", type=int, default=200)
     ap.add_argument("--engine", type=int, default=-1, choices=(-1, 0, 1),
                     help="-1 auto (persistent kernel when instantiated), 0 graph of kernels, 1 persistent")
-    ap.add_argument("--fuse-attn-wo", type=int, default=1, choices=(0, 1),
-                    help="graph engine: attention + Wo in one launch (1) or two (0)")
+    ap.add_argument("--fuse-attn-wo", type=int, default=1, choices=(0, 1, 2),
+                    help="graph engine: qkv + attention + Wo in one launch (2), attention + Wo (1), none (0)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -271,7 +271,8 @@ def main():
             "config": {"workload": w["desc"], "prompt_tokens": len(prompt), "max_seq_len": c.max_seq_len,
                        "kv_len_timed": [pos + 1, pos + args.steps], "batch": 1, "parallelism": f"replicas x{world}",
                        "engine": "persistent" if engine == 1 else
-                       ("graph, attention+Wo fused" if args.fuse_attn_wo else "graph")},
+                       {2: "graph, qkv+attention+Wo fused", 1: "graph, attention+Wo fused",
+                        0: "graph"}[model.get_option(L.OPT_FUSE_ATTN_WO)]},
             "roofline": roofline,
             "hbm_step": {"achieved_GBps": round(step_gbps, 1), "frac": round(step_gbps / HBM_PEAK_GBPS, 4),
                          "bytes_per_token": step_bytes // args.steps,

@@ -139,7 +139,8 @@ int xh_get_engine(const xh_ctx* ctx); /* the engine the next call will use */
 /* Device time (HIP events on the context's stream) of the last persistent-engine launch,
  * in microseconds: one launch covers a whole xh_prefill / xh_decode_greedy call. */
 int xh_last_launch_us(const xh_ctx* ctx, float* us);
-/* Debug timelines.  enable (bits): 1 = persistent engine, 2 = fused attention + Wo launches
+/* Debug timelines.  enable (bits): 1 = persistent engine, 2 = fused attention + Wo launches,
+ * 4 = fused qkv + attention + Wo launches ([workgroup][8] stamps, see qaw.h)
  * ([workgroup][4] stamps: start, attention done / hand-off passed, end; each launch
  * overwrites), 0 = off, -1 = unchanged.  Copies min(cap, *len) words of the last traced launch
  * to `out` first.  Persistent engine: for the launch's last token, workgroups {0, n_cu/2, n_cu-1} x [n_layers + 1][5 phases][2] device
@@ -164,10 +165,13 @@ size_t xh_active_bytes(const xh_ctx* ctx, size_t pos);
 /* Graph capture of the per-token step (default on).  Off = eager launches (debugging). */
 int xh_set_graphs(xh_ctx* ctx, int enable);
 
-/* Graph-engine variants.  XH_OPT_FUSE_ATTN_WO (default 1): attention and the Wo projection
- * (+ residual) in one launch with an in-launch hand-off; 0 = two launches.  Same math. */
+/* Graph-engine variants.  XH_OPT_FUSE_ATTN_WO (default 1): 2 = rmsnorm + Wq/Wk/Wv, attention
+ * and Wo (+ residual) in ONE launch with in-launch hand-offs (qaw.h); 1 = qkv launch, then
+ * attention + Wo in one launch (attn_wo.h); 0 = three launches.  Same math.  Level 2 falls
+ * back to 1 where the shape is not instantiated; xh_get_option reports the level in effect. */
 enum xh_option { XH_OPT_FUSE_ATTN_WO = 1 };
 int xh_set_option(xh_ctx* ctx, int option, int value);
+int xh_get_option(const xh_ctx* ctx, int option, int* value);
 
 /* ---- exposed-for-tests ops (src/model.h:286-316), host pointers in/out -------------- */
 /* matmul: xout[d] = W[d,n] @ x[n], W of `dtype` (src/infer.cpp:185-216). */

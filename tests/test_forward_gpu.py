@@ -20,16 +20,20 @@ FIXTURES = ["tiny_mistral_f16", "tiny_mistral_bf16", "tiny_mistral_f32", "tiny_m
             "tiny_mistral_f8_e5m2", "small_llama_f16"]
 
 
-# "graph": hipGraph of kernels per token (attention + Wo fused in one launch, the default);
-# "graph_split": the same with attention and Wo as two launches; "persistent": one persistent
-# kernel per call (xh_set_engine(1))
-ENGINES = ["graph", "graph_split", "persistent"]
+# "graph_qaw": hipGraph of kernels per token with rmsnorm + qkv, attention and Wo in ONE launch
+# (qaw.h, the default); "graph": qkv, then attention + Wo in one launch; "graph_split": three
+# launches; "persistent": one persistent kernel per call (xh_set_engine(1))
+ENGINES = ["graph_qaw", "graph", "graph_split", "persistent"]
+FUSE = {"graph_qaw": 2, "graph": 1, "graph_split": 0, "persistent": 1}
 
 
 def configure(gm, engine):
     gm.set_engine(1 if engine == "persistent" else 0)
-    gm.set_option(L.OPT_FUSE_ATTN_WO, 0 if engine == "graph_split" else 1)
+    gm.set_option(L.OPT_FUSE_ATTN_WO, FUSE[engine])
     assert gm.engine == (1 if engine == "persistent" else 0)
+    if engine != "persistent":
+        # the level in effect: every fixture's head shape is instantiated
+        assert gm.get_option(L.OPT_FUSE_ATTN_WO) == FUSE[engine]
 
 
 def tol(ref):

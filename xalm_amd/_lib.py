@@ -68,6 +68,7 @@ _SIGNATURES = {
     "xh_active_bytes": (_SZ, [_P, _SZ]),
     "xh_set_graphs": (_I, [_P, _I]),
     "xh_set_option": (_I, [_P, _I, _I]),
+    "xh_get_option": (_I, [_P, _I, ctypes.POINTER(_I)]),
     "xh_op_matmul": (_I, [_P, _P, _P, _I, _I, _I]),
     "xh_op_rmsnorm": (_I, [_P, _P, _P, _I, _I, ctypes.c_float]),
     "xh_op_rope": (_I, [_P, _I, _I, _I, ctypes.c_float, _I]),

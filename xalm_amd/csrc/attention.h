@@ -62,12 +62,30 @@ __device__ __forceinline__ void st_sc1(float* p, const float v) {
     __hip_atomic_store((uint32_t*)p, __builtin_bit_cast(uint32_t, v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+struct NoWait {
+    __device__ void operator()() const {}
+};
+// PARTIALS arrival: one relaxed agent-scope add on *done (after the partial is drained)
+struct AddArrive {
+    __device__ void operator()(unsigned* done) const {
+        __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+};
+
 // One workgroup of THREADS threads: KV head g, split s.  PARTIALS (attn_wo.h): every active
 // split stores its partial (o, m, l) write-through, drains, and adds 1 to *done; the
 // consumers merge (no ticket, no merge round trips inside the attention chain).
-template <int HD, int QPK, int THREADS, bool PARTIALS>
+// FUSED (qaw.h): q and this token's K/V row are produced inside the same launch.  The first
+// round of K/V rows is requested before `wait()` returns, except the rows this launch writes
+// (slot kv_pos, and the sink rows 0..kv_sink-1 that the qkv phase re-rotates): those, and q,
+// are read after the hand-off with sc1 loads only, so no stale copy of them can sit in this
+// CU's caches (MI355X_MICROARCH.md "Valid forms", consumer condition 1).
+// MINT: split floor (0 = the default of the mode); `arrive(done)` runs on thread 0.
+template <int HD, int QPK, int THREADS, bool PARTIALS, bool FUSED = false, int MINT = 0, class Wait = NoWait,
+          class Arrive = AddArrive>
 __device__ __forceinline__ void attn_block(const AttnArgs& a, const int g, const int s, char* smem, unsigned* done,
-                                           unsigned long long* dbg = nullptr) {
+                                           unsigned long long* dbg = nullptr, const Wait& wait = Wait(),
+                                           const Arrive& arrive = Arrive()) {
 #define ATTN_STAMP(k) \
     do { if (dbg && threadIdx.x == 0) dbg[k] = __builtin_amdgcn_s_memrealtime(); } while (0)
     constexpr int WAVES = THREADS / 64;
@@ -80,7 +98,7 @@ __device__ __forceinline__ void attn_block(const AttnArgs& a, const int g, const
     int* flag = (int*)(ml + 2 * QPK);
 
     const int kv_len = a.sp->kv_len;
-    constexpr int MIN_T = PARTIALS ? attn_min_t_partials(HD, THREADS) : ATTN_MIN_T;
+    constexpr int MIN_T = MINT ? MINT : PARTIALS ? attn_min_t_partials(HD, THREADS) : ATTN_MIN_T;
     const int T = attn_split_len(kv_len, a.nsplit, MIN_T);
     const int t0 = s * T;
     if (t0 >= kv_len) return;
@@ -91,22 +109,51 @@ __device__ __forceinline__ void attn_block(const AttnArgs& a, const int g, const
     const int sub = tid % LPR, rr = tid / LPR;
     const float scale = 1.0f / sqrtf((float)HD);  // src/infer.cpp:338
     const size_t col = (size_t)g * HD + sub * 8;
+    // FUSED: rows written in this launch
+    const int kv_pos = FUSED ? a.sp->kv_pos : -1;
+    const int kv_sink = FUSED ? a.sp->kv_sink : 0;
+    auto fresh = [&](const int t) { return FUSED && (t == kv_pos || t < kv_sink); };
+    auto ld_kv = [&](const uint16_t* base, const int t) {
+        const size_t off = ((size_t)t * a.kv_dim + col) * 2;
+        if (fresh(t)) return ld_sc1_x4(base, (uint32_t)off);
+        return *(const u32x4*)((const char*)base + off);
+    };
 
     // ---- first round of K and V rows, requested before anything else ----
     u32x4 kr[ATTN_PREF], vr[ATTN_PREF];
 #pragma unroll
     for (int p = 0; p < ATTN_PREF; p++) {
         const int t = t0 + rr + p * RPP;
-        if (t < t1) {
+        if (t < t1 && !fresh(t)) {
             kr[p] = *(const u32x4*)(a.kc + (size_t)t * a.kv_dim + col);
             vr[p] = *(const u32x4*)(a.vc + (size_t)t * a.kv_dim + col);
         }
     }
     float qv[QPK][8];
+    if (FUSED) {
+        wait();
+#pragma unroll
+        for (int p = 0; p < ATTN_PREF; p++) {
+            const int t = t0 + rr + p * RPP;
+            if (t < t1 && fresh(t)) {
+                kr[p] = ld_kv(a.kc, t);
+                vr[p] = ld_kv(a.vc, t);
+            }
+        }
+    }
 #pragma unroll
     for (int h = 0; h < QPK; h++) {
-        const float4* qp = (const float4*)(a.q + (size_t)(g * QPK + h) * HD + sub * 8);
-        const float4 q0 = qp[0], q1 = qp[1];
+        const size_t qo = (size_t)(g * QPK + h) * HD + sub * 8;
+        float4 q0, q1;
+        if (FUSED) {
+            const u32x4 u0 = ld_sc1_x4(a.q, (uint32_t)(qo * 4)), u1 = ld_sc1_x4(a.q, (uint32_t)(qo * 4 + 16));
+            q0 = make_float4(bits_f32(u0.x), bits_f32(u0.y), bits_f32(u0.z), bits_f32(u0.w));
+            q1 = make_float4(bits_f32(u1.x), bits_f32(u1.y), bits_f32(u1.z), bits_f32(u1.w));
+        } else {
+            const float4* qp = (const float4*)(a.q + qo);
+            q0 = qp[0];
+            q1 = qp[1];
+        }
         qv[h][0] = q0.x; qv[h][1] = q0.y; qv[h][2] = q0.z; qv[h][3] = q0.w;
         qv[h][4] = q1.x; qv[h][5] = q1.y; qv[h][6] = q1.z; qv[h][7] = q1.w;
     }
@@ -134,7 +181,7 @@ __device__ __forceinline__ void attn_block(const AttnArgs& a, const int g, const
 #pragma unroll
         for (int p = 0; p < ATTN_PREF; p++) {
             const int t = base + rr + p * RPP;
-            if (t < t1) kk[p] = *(const u32x4*)(a.kc + (size_t)t * a.kv_dim + col);
+            if (t < t1) kk[p] = ld_kv(a.kc, t);
         }
 #pragma unroll
         for (int p = 0; p < ATTN_PREF; p++) {
@@ -189,7 +236,7 @@ __device__ __forceinline__ void attn_block(const AttnArgs& a, const int g, const
 #pragma unroll
         for (int p = 0; p < ATTN_PREF; p++) {
             const int t = base + rr + p * RPP;
-            if (t < t1) vv[p] = *(const u32x4*)(a.vc + (size_t)t * a.kv_dim + col);
+            if (t < t1) vv[p] = ld_kv(a.vc, t);
         }
 #pragma unroll
         for (int p = 0; p < ATTN_PREF; p++) {
@@ -253,7 +300,7 @@ __device__ __forceinline__ void attn_block(const AttnArgs& a, const int g, const
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         ATTN_STAMP(5);
-        if (tid == 0) __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (tid == 0) arrive(done);
         return;
     }
     if (n_active == 1) {

@@ -42,7 +42,7 @@ __host__ __device__ constexpr size_t aw_image_bytes(const int n) {
 // x image of the Wo rows = the merged attention output.  wts: LDS [n_heads][n_active] weights,
 // [n_heads] denominators, then the (m, l) pairs [n_active][n_heads][2].  The partial-o loads
 // of a thread's first float4 are issued together with the (m, l) loads (one round trip).
-template <int E, int HD>
+template <int E, int HD, int THREADS = AW_THREADS>
 __device__ __forceinline__ void aw_stage_merged(const AttnArgs& aa, const int n, const int n_active, float4* xs4,
                                                 float* wts) {
     constexpr int MAXS = 4;  // prefetched partials per thread (registers beside the Wo rows)
@@ -59,13 +59,13 @@ __device__ __forceinline__ void aw_stage_merged(const AttnArgs& aa, const int n,
     }
     float* ml = wts + nh * (n_active + 1);
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)aa.part_ml, 0, 0x7fffffff, 0x00020000);
-    for (int i = tid; i < n_active * nh; i += AW_THREADS) {
+    for (int i = tid; i < n_active * nh; i += THREADS) {
         ml[2 * i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, i * 8, 0, 16));  // sc1
         ml[2 * i + 1] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, i * 8 + 4, 0, 16));
     }
     __syncthreads();
     // per head: weights e^{m_s - M} and the denominator sum_s e^{m_s - M} l_s
-    for (int h = tid; h < nh; h += AW_THREADS) {
+    for (int h = tid; h < nh; h += THREADS) {
         float M = -FLT_MAX;
         for (int j = 0; j < n_active; j++) M = fmaxf(M, ml[2 * (j * nh + h)]);
         float den = 0.f;
@@ -77,7 +77,7 @@ __device__ __forceinline__ void aw_stage_merged(const AttnArgs& aa, const int n,
         wts[nh * n_active + h] = den;
     }
     __syncthreads();
-    for (int i = tid; i < n4; i += AW_THREADS) {
+    for (int i = tid; i < n4; i += THREADS) {
         const int h = (4 * i) / HD;
         const float* w = wts + h * n_active;
         float4 num = make_float4(0.f, 0.f, 0.f, 0.f);

@@ -202,6 +202,15 @@ __device__ __forceinline__ void rows_reduce_scatter(float (&v)[N]) {
 __device__ __forceinline__ float wave_sum(float v) { return group_reduce<64, OpSum>(v); }
 __device__ __forceinline__ float wave_max(float v) { return group_reduce<64, OpMax>(v); }
 
+// Orderable key of (logit, index) for Sampler::sample_argmax (src/sampler.cpp:19-30): a larger
+// logit wins, then the smaller index (the first maximum); 0 = no candidate.
+__device__ __forceinline__ unsigned long long argmax_key(const float v, const int idx) {
+    uint32_t u = __builtin_bit_cast(uint32_t, v);
+    u = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+    return ((unsigned long long)u << 32) | (uint32_t)(~(uint32_t)idx);
+}
+__device__ __forceinline__ int argmax_key_index(const unsigned long long k) { return k ? (int)(~(uint32_t)k) : 0; }
+
 // Per-token dynamic scalars, read by every kernel of a captured graph.
 // kv_sink / kv_pos / kv_len follow src/infer.cpp:611-613.
 struct StepParams {

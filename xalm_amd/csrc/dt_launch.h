@@ -7,6 +7,7 @@
 
 #include "attn_wo.h"
 #include "persistent.h"
+#include "qaw.h"
 
 namespace xalm {
 
@@ -36,6 +37,20 @@ XALM_AW_DECL(6)
 XALM_AW_DECL(7)
 XALM_AW_DECL(9)
 #undef XALM_AW_DECL
+// qkv + attention + Wo in one launch (qaw.h) for weight dtype DT (wq/wk/wv and Wo share it):
+// grid = attention workgroups + row workgroups = 2 x n_cu.  Returns 0, or XH_E_INVALID when
+// the shape is not instantiated or does not fit two workgroups per CU (caller falls back).
+#define XALM_QAW_DECL(DT)                                                                                    \
+    int qaw_launch_dt##DT(const GemvArgs& qa, const AttnArgs& aa, const GemvArgs& wa, int head_dim, int qpk, \
+                          int n_kv_heads, int t_max, int n_cu, const QawSync& sy, hipStream_t stream);
+XALM_QAW_DECL(1)
+XALM_QAW_DECL(2)
+XALM_QAW_DECL(3)
+XALM_QAW_DECL(6)
+XALM_QAW_DECL(7)
+XALM_QAW_DECL(9)
+#undef XALM_QAW_DECL
+
 inline bool aw_instantiated(int hd, int qpk) {
     return (hd == 128 && (qpk == 4 || qpk == 8)) || (hd == 64 && qpk == 4) || (hd == 16 && qpk == 2);
 }

@@ -77,6 +77,25 @@ int aw_go(const AttnArgs& aa, const GemvArgs& ga, int n_kv_heads, int t_max, uns
     return hipGetLastError() == hipSuccess ? 0 : XH_E_HIP;
 }
 
+template <int DT, int HD, int QPK>
+int qaw_go(const GemvArgs& qa, const AttnArgs& aa, const GemvArgs& wa, int n_kv_heads, int t_max, int n_cu,
+           const QawSync& sy, hipStream_t stream) {
+    const size_t smem = qaw_smem_bytes<DT>(HD, QPK, t_max, aa.nsplit, qa.n, wa.n, aa.n_heads);
+    if (smem > 80 * 1024) return XH_E_INVALID;  // two workgroups per CU
+    auto k = qkv_attn_wo_kernel<DT, HD, QPK>;
+    static int per_cu = -1;
+    if (per_cu < 0) {
+        if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024) != hipSuccess)
+            return XH_E_HIP;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, QAW_THREADS, 80 * 1024) != hipSuccess) per_cu = 0;
+    }
+    if (per_cu < 2) return XH_E_INVALID;
+    const int grid = 2 * n_cu;
+    if (n_kv_heads * aa.nsplit >= grid) return XH_E_INVALID;
+    hipLaunchKernelGGL(k, dim3(grid), dim3(QAW_THREADS), smem, stream, qa, aa, wa, n_kv_heads, sy);
+    return hipGetLastError() == hipSuccess ? 0 : XH_E_HIP;
+}
+
 }  // namespace
 
 #define XALM_CAT2(a, b) a##b
@@ -88,6 +107,16 @@ int XALM_CAT(aw_launch_dt, PK_DT)(const AttnArgs& aa, const GemvArgs& ga, int he
     if (head_dim == 128 && qpk == 8) return aw_go<PK_DT, 128, 8>(aa, ga, n_kv_heads, t_max, sync, max_waves, stream, trace);
     if (head_dim == 64 && qpk == 4) return aw_go<PK_DT, 64, 4>(aa, ga, n_kv_heads, t_max, sync, max_waves, stream, trace);
     if (head_dim == 16 && qpk == 2) return aw_go<PK_DT, 16, 2>(aa, ga, n_kv_heads, t_max, sync, max_waves, stream, trace);
+    return XH_E_INVALID;
+}
+
+int XALM_CAT(qaw_launch_dt, PK_DT)(const GemvArgs& qa, const AttnArgs& aa, const GemvArgs& wa, int head_dim,
+                                   int qpk, int n_kv_heads, int t_max, int n_cu, const QawSync& sy,
+                                   hipStream_t stream) {
+    if (head_dim == 128 && qpk == 4) return qaw_go<PK_DT, 128, 4>(qa, aa, wa, n_kv_heads, t_max, n_cu, sy, stream);
+    if (head_dim == 128 && qpk == 8) return qaw_go<PK_DT, 128, 8>(qa, aa, wa, n_kv_heads, t_max, n_cu, sy, stream);
+    if (head_dim == 64 && qpk == 4) return qaw_go<PK_DT, 64, 4>(qa, aa, wa, n_kv_heads, t_max, n_cu, sy, stream);
+    if (head_dim == 16 && qpk == 2) return qaw_go<PK_DT, 16, 2>(qa, aa, wa, n_kv_heads, t_max, n_cu, sy, stream);
     return XH_E_INVALID;
 }
 

@@ -7,6 +7,8 @@
 //             EPI_GLU     : hb = act(W1 x) * (W3 x) (:468-488), W1/W3 rows interleaved
 //             EPI_RESID   : x += W x (:447-452, :490-494)
 //             EPI_STORE   : y = W x (logits, :637)
+//             EPI_LOGITS  : EPI_STORE + one argmax candidate per workgroup (Sampler::sample_argmax,
+//                           src/sampler.cpp:19-30), for the device decode loop
 //
 // HBM layout: W row-major [rows][n] exactly as the .xalm tensor (HF [out,in]).  One wave
 // owns ROWS consecutive rows; lane l streams 16-byte chunks l, l+64, l+128, ... of each row
@@ -17,12 +19,14 @@
 // no MFMA: batch-1 matvec is HBM-bound at ~1 FLOP per weight byte.
 #pragma once
 
+#include <float.h>
+
 #include "common.h"
 
 namespace xalm {
 
 enum { PRO_PLAIN = 0, PRO_RMSNORM = 1 };
-enum { EPI_STORE = 0, EPI_RESID = 1, EPI_QKV = 2, EPI_GLU = 3 };
+enum { EPI_STORE = 0, EPI_RESID = 1, EPI_QKV = 2, EPI_GLU = 3, EPI_LOGITS = 4 };
 
 constexpr int LDS_HEAD_BYTES = 64;  // block-reduction scratch in front of the x image
 
@@ -63,6 +67,7 @@ struct GemvArgs {
     int act;
     const StepParams* sp;
     unsigned long long* trace;  // debug (null = off): per workgroup [4] start, x staged, rows done
+    unsigned long long* cand;   // EPI_LOGITS: [gridDim.x] argmax_key of the workgroup's best logit
 };
 
 // agent-scope relaxed (sc1: L1-bypassing, write-through) accesses for data handed between
@@ -195,8 +200,20 @@ __device__ __forceinline__ void epi_st(float* p, const float v) {
     else *p = v;
 }
 template <int EPI, int ROWS, bool SC1 = false>
-__device__ __forceinline__ void gemv_epilogue(const GemvArgs& a, const int row0, const float* acc) {
-    if (EPI == EPI_STORE) {
+__device__ __forceinline__ void gemv_epilogue(const GemvArgs& a, const int row0, const float* acc,
+                                              unsigned long long* best = nullptr) {
+    if (EPI == EPI_LOGITS) {
+#pragma unroll
+        for (int r = 0; r < ROWS; r++)
+            if (row0 + r < a.rows) {
+                a.out[row0 + r] = acc[r];
+                // only logits > FLT_MIN compete (max_val starts at FLT_MIN, strict '>')
+                if (acc[r] > FLT_MIN) {
+                    const unsigned long long k = argmax_key(acc[r], row0 + r);
+                    *best = k > *best ? k : *best;
+                }
+            }
+    } else if (EPI == EPI_STORE) {
 #pragma unroll
         for (int r = 0; r < ROWS; r++)
             if (row0 + r < a.rows) epi_st<SC1>(a.out + row0 + r, acc[r]);
@@ -306,7 +323,7 @@ __device__ __forceinline__ void gemv_prefetch(const GemvArgs& a, const int g, co
 // Chunks [it, n) of group g into acc, then the wave reduction and the epilogue.
 template <int DT, int EPI, class S, bool SC1 = false>
 __device__ __forceinline__ void gemv_group(const GemvArgs& a, const int g, const int lane, const float4* xs4, float* acc,
-                                           int it) {
+                                           int it, unsigned long long* best = nullptr) {
     constexpr int ROWS = S::ROWS, U = S::U;
     constexpr int E = WDec<DT>::E;
     const int n = a.n;
@@ -321,7 +338,7 @@ __device__ __forceinline__ void gemv_group(const GemvArgs& a, const int g, const
     if (it < n_it && (it * 64 + lane) * E < n) gemv_chunk<DT, ROWS, 1, S::NT>(wrow, rstride, xs4, it, lane, acc);
 #pragma unroll
     for (int r = 0; r < ROWS; r++) acc[r] = wave_sum(acc[r]);
-    if (lane == 0) gemv_epilogue<EPI, ROWS, SC1>(a, g * ROWS, acc);
+    if (lane == 0) gemv_epilogue<EPI, ROWS, SC1>(a, g * ROWS, acc, best);
 }
 
 // Groups g, g + total_waves, ... of this wave against the staged x image.  FIRST: the first
@@ -329,21 +346,22 @@ __device__ __forceinline__ void gemv_group(const GemvArgs& a, const int g, const
 // that group is peeled so `pre` is dead in the loop.
 template <int DT, int EPI, class S, bool FIRST, bool SC1 = false>
 __device__ __forceinline__ void gemv_rows(const GemvArgs& a, int g, const int total_waves, const int lane,
-                                          const float4* xs4, const u32x4 (&pre)[S::U][S::ROWS]) {
+                                          const float4* xs4, const u32x4 (&pre)[S::U][S::ROWS],
+                                          unsigned long long* best = nullptr) {
     const int n_groups = gemv_groups<S>(a);
     if (FIRST) {
         float acc[S::ROWS];
 #pragma unroll
         for (int r = 0; r < S::ROWS; r++) acc[r] = 0.f;
         gemv_compute<DT, S::ROWS, S::U>(pre, xs4, 0, lane, acc);
-        gemv_group<DT, EPI, S, SC1>(a, g, lane, xs4, acc, S::U);
+        gemv_group<DT, EPI, S, SC1>(a, g, lane, xs4, acc, S::U, best);
         g += total_waves;
     }
     for (; g < n_groups; g += total_waves) {
         float acc[S::ROWS];
 #pragma unroll
         for (int r = 0; r < S::ROWS; r++) acc[r] = 0.f;
-        gemv_group<DT, EPI, S, SC1>(a, g, lane, xs4, acc, 0);
+        gemv_group<DT, EPI, S, SC1>(a, g, lane, xs4, acc, 0, best);
     }
 }
 
@@ -422,6 +440,7 @@ __global__ __launch_bounds__(S::THREADS, S::MINW) void gemv_kernel(const GemvArg
     const int wid = threadIdx.x >> 6;
     const int g = blockIdx.x * S::WAVES + wid;
     if (a.trace && threadIdx.x == 0) a.trace[4 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+    unsigned long long best = 0;  // EPI_LOGITS: this wave's best candidate (lane 0)
 
     if constexpr (S::PF) {
         float4 xv[S::XN], nw[S::XN];
@@ -435,15 +454,28 @@ __global__ __launch_bounds__(S::THREADS, S::MINW) void gemv_kernel(const GemvArg
         if (EPI == EPI_QKV && blockIdx.x == 0) rotate_sinks<S::THREADS>(a, a.sp->kv_sink);
         __syncthreads();
         if (a.trace && threadIdx.x == 0) a.trace[4 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
-        if (prefetched) gemv_rows<DT, EPI, S, true>(a, g, gridDim.x * S::WAVES, lane, xs4, pre);
-        else gemv_rows<DT, EPI, S, false>(a, g, gridDim.x * S::WAVES, lane, xs4, pre);
+        if (prefetched) gemv_rows<DT, EPI, S, true>(a, g, gridDim.x * S::WAVES, lane, xs4, pre, &best);
+        else gemv_rows<DT, EPI, S, false>(a, g, gridDim.x * S::WAVES, lane, xs4, pre, &best);
     } else {
         stage_x<E, PRO, S::THREADS>(a, xs4, red);
         if (EPI == EPI_QKV && blockIdx.x == 0) rotate_sinks<S::THREADS>(a, a.sp->kv_sink);
         __syncthreads();
         if (a.trace && threadIdx.x == 0) a.trace[4 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
         u32x4 none[S::U][S::ROWS];
-        gemv_rows<DT, EPI, S, false>(a, g, gridDim.x * S::WAVES, lane, xs4, none);
+        gemv_rows<DT, EPI, S, false>(a, g, gridDim.x * S::WAVES, lane, xs4, none, &best);
+    }
+    if constexpr (EPI == EPI_LOGITS) {
+        // the workgroup's candidate: lane 0 of each wave holds its best
+        unsigned long long* kb = (unsigned long long*)smem;  // the rms scratch is free again
+        __syncthreads();
+        if (lane == 0) kb[wid] = best;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            unsigned long long bb = 0;
+#pragma unroll
+            for (int w = 0; w < S::WAVES; w++) bb = kb[w] > bb ? kb[w] : bb;
+            a.cand[blockIdx.x] = bb;
+        }
     }
     if (a.trace) {
         __syncthreads();

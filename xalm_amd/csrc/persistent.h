@@ -101,12 +101,7 @@ __device__ __forceinline__ const struct PkArgs* pk_args() {
 
 __device__ __forceinline__ uint64_t pk_now() { return __builtin_amdgcn_s_memrealtime(); }
 
-// orderable key of (logit, index): larger logit first, then smaller index (first max wins)
-__device__ __forceinline__ unsigned long long pk_key(const float v, const int idx) {
-    uint32_t u = __builtin_bit_cast(uint32_t, v);
-    u = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
-    return ((unsigned long long)u << 32) | (uint32_t)(~(uint32_t)idx);
-}
+__device__ __forceinline__ unsigned long long pk_key(const float v, const int idx) { return argmax_key(v, idx); }
 
 // publish: every wave's sc1 stores drained, then one add (after a workgroup barrier)
 __device__ __forceinline__ void pk_signal(unsigned* c, const unsigned add = 1) {

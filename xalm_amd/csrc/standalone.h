@@ -2,6 +2,8 @@
 // Included by xalm_hip.hip only: non-template kernels must live in one translation unit.
 #pragma once
 
+#include <float.h>
+
 #include "gemv.h"
 
 namespace xalm {
@@ -29,9 +31,75 @@ __global__ void rope_kernel(float* vec, int d, int head_dim, int pos, const floa
 }
 
 // Model::_copy_embedding (src/infer.cpp:553-602): x = dec(embed[token, :])
-__global__ void embed_kernel(const void* emb, int dtype, int dim, float* x, const StepParams* sp) {
+// also advances the forward-step epoch of the fused launches' monotonic counters (qaw.h)
+__global__ void embed_kernel(const void* emb, int dtype, int dim, float* x, const StepParams* sp, unsigned* epoch) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i == 0 && epoch) *epoch += 1;
     if (i < dim) x[i] = dec1(dtype, emb, (size_t)sp->token * dim + i);
+}
+
+// Greedy decode step head: argmax over the lm_head workgroups' candidates (Sampler::
+// sample_argmax, src/sampler.cpp:19-30: the first maximum among logits > FLT_MIN, else token
+// 0), the decode-loop bookkeeping of argmax_advance (tokens[step], step, token, positions,
+// src/infer.cpp:611-613), the epoch, and x = embed[token] (Model::_copy_embedding,
+// src/infer.cpp:553-602), in one 1024-thread workgroup.
+constexpr int ARGMAX_CANDS = 1024;
+__global__ __launch_bounds__(1024) void argmax_embed_kernel(const unsigned long long* cand, StepParams* sp,
+                                                            int* tokens, int cap, const void* emb, int dtype,
+                                                            int dim, float* x, unsigned* epoch) {
+    __shared__ unsigned long long kb[16];
+    __shared__ int tok_s;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    unsigned long long best = cand[tid];  // ARGMAX_CANDS == blockDim.x
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long other = __shfl_xor(best, o, 64);
+        best = other > best ? other : best;
+    }
+    if (lane == 0) kb[wid] = best;
+    __syncthreads();
+    if (tid == 0) {
+        unsigned long long bb = 0;
+#pragma unroll
+        for (int w = 0; w < 16; w++) bb = kb[w] > bb ? kb[w] : bb;
+        const int tok = argmax_key_index(bb);
+        if (sp->step < cap) tokens[sp->step] = tok;
+        sp->step += 1;
+        sp->token = tok;
+        step_positions(sp, sp->pos_next);
+        sp->pos_next += 1;
+        if (epoch) *epoch += 1;
+        tok_s = tok;
+    }
+    __syncthreads();
+    const size_t base = (size_t)tok_s * dim;
+    for (int i = tid; i < dim; i += 1024) x[i] = dec1(dtype, emb, base + i);
+}
+
+// Candidates from logits already on the device (the first greedy step after logits that no
+// EPI_LOGITS launch produced): cand[0] = best key, the rest 0.
+__global__ __launch_bounds__(1024) void logits_cand_kernel(const float* logits, int vocab, unsigned long long* cand) {
+    __shared__ unsigned long long kb[16];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    unsigned long long best = 0;
+    for (int i = tid; i < vocab; i += 1024) {
+        const float v = logits[i];
+        if (v > FLT_MIN) {
+            const unsigned long long k = argmax_key(v, i);
+            best = k > best ? k : best;
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long other = __shfl_xor(best, o, 64);
+        best = other > best ? other : best;
+    }
+    if (lane == 0) kb[wid] = best;
+    __syncthreads();
+    unsigned long long bb = 0;
+#pragma unroll
+    for (int w = 0; w < 16; w++) bb = kb[w] > bb ? kb[w] : bb;
+    cand[tid] = tid == 0 ? bb : 0ull;
 }
 
 }  // namespace xalm

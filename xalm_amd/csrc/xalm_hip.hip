@@ -82,11 +82,18 @@ struct xh_ctx {
     StepParams* sp = nullptr;       // device
     StepParams* sp_host = nullptr;  // pinned
     int* dec_tokens = nullptr;      // device, decode loop output
+    unsigned long long* cand = nullptr;  // device [ARGMAX_CANDS]: lm_head workgroups' argmax keys
+    bool cand_valid = false;        // cand describes the logits on the device
     int dec_cap = 0;
     int nsplit = 1, t_max = 16;
     // fused attention + Wo launch (attn_wo.h): per-layer hand-off words [n_layers][4]
     bool fuse_attn_wo = true;
     unsigned* aw_sync = nullptr;
+    // qkv + attention + Wo in one launch (qaw.h), used when fuse_level == 2 and instantiated
+    int fuse_level = 1;  // 2 (qaw.h) measured slower end to end on MI355X: see DESIGN.md
+    unsigned* qaw_sync = nullptr;  // [n_layers][QAW_LAYER_WORDS] counters, then epoch, err
+    int qaw_nsplit = 1, qaw_t_max = 16;
+    bool qaw_ok = true;            // cleared when a launch reports the shape unsupported
     int t_max_aw = 16;
     bool use_graphs = true;
     hipGraphExec_t g_logits = nullptr, g_hydrate = nullptr, g_decode = nullptr;
@@ -108,12 +115,18 @@ struct xh_ctx {
     unsigned long long* pk_trace = nullptr;  // device [PK_TRACE_WG][pk_trace_len]
     bool pk_trace_on = false;
     bool aw_trace_on = false;  // fused attention + Wo launches write pk_trace (debug)
+    bool qaw_trace_on = false;  // fused qkv + attention + Wo launches write pk_trace (debug)
 
     uint16_t* kcache(int l) { return kv + (size_t)l * 2 * c.max_seq_len * kv_dim; }
     uint16_t* vcache(int l) { return kcache(l) + (size_t)c.max_seq_len * kv_dim; }
 };
 
 namespace {
+
+constexpr int QAW_LAYER_WORDS = (2 * CHAIN_SHARDS + 1) * CHAIN_SHARD_STRIDE;
+unsigned* qaw_epoch(const xh_ctx* ctx) { return ctx->qaw_sync + (size_t)ctx->c.n_layers * QAW_LAYER_WORDS; }
+int* qaw_err(const xh_ctx* ctx) { return (int*)(qaw_epoch(ctx) + CHAIN_SHARD_STRIDE); }
+size_t qaw_words(const xh_config& c) { return (size_t)c.n_layers * QAW_LAYER_WORDS + 2 * CHAIN_SHARD_STRIDE; }
 
 int set_err(xh_ctx* ctx, int code, const char* fmt, ...) {
     char buf[1024];
@@ -282,7 +295,7 @@ GemvArgs cls_args(xh_ctx* ctx) {
     a.w = ctx->wcls; a.row_bytes = (size_t)ctx->c.dim * dtype_size(ctx->wcls_dt);
     a.n = ctx->c.dim; a.rows = ctx->c.vocab_size; a.x = ctx->x;
     a.norm_w = ctx->final_norm; a.norm_dtype = ctx->final_norm_dt; a.eps = ctx->c.norm_eps;
-    a.out = ctx->logits; a.sp = ctx->sp;
+    a.out = ctx->logits; a.sp = ctx->sp; a.cand = ctx->cand;
     return a;
 }
 AttnArgs attn_args(xh_ctx* ctx, int l) {
@@ -348,8 +361,38 @@ int launch_attn_wo(xh_ctx* ctx, int l, hipStream_t s) {
     }
 }
 
+// qkv + attention + Wo launch of layer l; XH_E_INVALID = shape not instantiated (fall back)
+int launch_qaw(xh_ctx* ctx, int l, hipStream_t s) {
+    const LayerW& w = ctx->L[l];
+    if (w.qkv_dt != w.wo_dt) return XH_E_INVALID;
+    AttnArgs aa = attn_args(ctx, l);
+    aa.nsplit = ctx->qaw_nsplit;
+    const GemvArgs qa = qkv_args(ctx, l), wa = wo_args(ctx, l);
+    QawSync sy{};
+    sy.qkv = ctx->qaw_sync + (size_t)l * QAW_LAYER_WORDS;
+    sy.heads = sy.qkv + CHAIN_SHARDS * CHAIN_SHARD_STRIDE;
+    sy.epoch = qaw_epoch(ctx);
+    sy.err = qaw_err(ctx);
+    sy.trace = ctx->qaw_trace_on ? ctx->pk_trace : nullptr;
+    const int hd = ctx->c.head_dim, qpk = ctx->qpk, nkv = ctx->c.n_kv_heads, tm = ctx->qaw_t_max, ncu = ctx->n_cu;
+    switch (w.qkv_dt) {
+        case XH_F32: return qaw_launch_dt1(qa, aa, wa, hd, qpk, nkv, tm, ncu, sy, s);
+        case XH_F16: return qaw_launch_dt2(qa, aa, wa, hd, qpk, nkv, tm, ncu, sy, s);
+        case XH_BF16: return qaw_launch_dt3(qa, aa, wa, hd, qpk, nkv, tm, ncu, sy, s);
+        case XH_F8_E4M3: return qaw_launch_dt6(qa, aa, wa, hd, qpk, nkv, tm, ncu, sy, s);
+        case XH_F8_E5M2: return qaw_launch_dt7(qa, aa, wa, hd, qpk, nkv, tm, ncu, sy, s);
+        case XH_Q8: return qaw_launch_dt9(qa, aa, wa, hd, qpk, nkv, tm, ncu, sy, s);
+        default: return XH_E_INVALID;
+    }
+}
+
 // a fused hand-off that timed out leaves its sticky flag: report it (after the stream sync)
 int check_aw(xh_ctx* ctx) {
+    {
+        int e = 0;
+        HIP_TRY(ctx, hipMemcpy(&e, qaw_err(ctx), sizeof(int), hipMemcpyDeviceToHost));
+        if (e) return set_err(ctx, XH_E_HIP, "qkv -> attention -> Wo hand-off timed out");
+    }
     if (!ctx->fuse_attn_wo) return 0;
     std::vector<unsigned> h((size_t)ctx->c.n_layers * 4);
     HIP_TRY(ctx, hipMemcpy(h.data(), ctx->aw_sync, h.size() * sizeof(unsigned), hipMemcpyDeviceToHost));
@@ -358,13 +401,25 @@ int check_aw(xh_ctx* ctx) {
     return 0;
 }
 
-int enqueue_step(xh_ctx* ctx, hipStream_t s, bool with_logits) {
+// greedy: the token is the argmax of the previous step's logits (argmax_embed_kernel)
+int enqueue_step(xh_ctx* ctx, hipStream_t s, bool with_logits, bool greedy = false) {
     const xh_config& c = ctx->c;
     const int mb = ctx->max_gemv_waves;
-    hipLaunchKernelGGL(embed_kernel, dim3((c.dim + 255) / 256), dim3(256), 0, s, (const void*)ctx->embed,
-                       ctx->embed_dt, c.dim, ctx->x, (const StepParams*)ctx->sp);
+    if (greedy)
+        hipLaunchKernelGGL(argmax_embed_kernel, dim3(1), dim3(ARGMAX_CANDS), 0, s, (const unsigned long long*)ctx->cand,
+                           ctx->sp, ctx->dec_tokens, ctx->dec_cap, (const void*)ctx->embed, ctx->embed_dt, c.dim,
+                           ctx->x, qaw_epoch(ctx));
+    else
+        hipLaunchKernelGGL(embed_kernel, dim3((c.dim + 255) / 256), dim3(256), 0, s, (const void*)ctx->embed,
+                           ctx->embed_dt, c.dim, ctx->x, (const StepParams*)ctx->sp, qaw_epoch(ctx));
     for (int l = 0; l < c.n_layers; l++) {
         const LayerW& w = ctx->L[l];
+        if (ctx->fuse_level >= 2 && ctx->qaw_ok && aw_instantiated(c.head_dim, ctx->qpk)) {
+            const int rc = launch_qaw(ctx, l, s);
+            if (rc == 0) goto mlp;
+            if (rc != XH_E_INVALID) return set_err(ctx, rc, "layer %d: qkv + attention + Wo launch failed", l);
+            ctx->qaw_ok = false;  // not instantiated / does not fit: the two-launch form from now on
+        }
         if (!launch_gemv<PRO_RMSNORM, EPI_QKV>(w.qkv_dt, qkv_args(ctx, l), s, mb))
             return set_err(ctx, XH_E_INVALID, "layer %d: unsupported qkv dtype %d", l, w.qkv_dt);
         if (use_attn_wo(ctx, l)) {
@@ -376,13 +431,14 @@ int enqueue_step(xh_ctx* ctx, hipStream_t s, bool with_logits) {
             if (!launch_gemv<PRO_PLAIN, EPI_RESID>(w.wo_dt, wo_args(ctx, l), s, mb))
                 return set_err(ctx, XH_E_INVALID, "layer %d: unsupported wo dtype", l);
         }
+    mlp:
         if (!launch_gemv<PRO_RMSNORM, EPI_GLU>(w.w13_dt, w13_args(ctx, l), s, mb))
             return set_err(ctx, XH_E_INVALID, "layer %d: unsupported w1/w3 dtype", l);
         if (!launch_gemv<PRO_PLAIN, EPI_RESID>(w.w2_dt, w2_args(ctx, l), s, mb))
             return set_err(ctx, XH_E_INVALID, "layer %d: unsupported w2 dtype", l);
     }
     if (with_logits) {
-        if (!launch_gemv<PRO_RMSNORM, EPI_STORE>(ctx->wcls_dt, cls_args(ctx), s, mb))
+        if (!launch_gemv<PRO_RMSNORM, EPI_LOGITS>(ctx->wcls_dt, cls_args(ctx), s, mb))
             return set_err(ctx, XH_E_INVALID, "unsupported wcls dtype");
     }
     HIP_TRY(ctx, hipGetLastError());
@@ -448,6 +504,7 @@ bool use_persistent(xh_ctx* ctx) {
 // One persistent launch: n_prompt tokens from `prompt` (host), then n_gen greedy tokens.
 int run_persistent(xh_ctx* ctx, const int* prompt, int n_prompt, int n_gen, int pos0, int logits_last, int stop_a,
                    int stop_b, int* n_done_out) {
+    ctx->cand_valid = false;  // its logits come without lm_head candidates
     const xh_config& c = ctx->c;
     int dt, dtc, ndt;
     if (!pk_dtypes(ctx, &dt, &dtc, &ndt))
@@ -517,11 +574,7 @@ int capture(xh_ctx* ctx, int kind, hipGraphExec_t* out) {
     hipGraph_t g = nullptr;
     HIP_TRY(ctx, hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal));
     int rc = 0;
-    if (kind == 2) {
-        hipLaunchKernelGGL(argmax_advance_kernel, dim3(1), dim3(1024), 0, ctx->stream, (const float*)ctx->logits,
-                           ctx->c.vocab_size, ctx->sp, ctx->dec_tokens, ctx->dec_cap);
-    }
-    rc = enqueue_step(ctx, ctx->stream, kind != 1);
+    rc = enqueue_step(ctx, ctx->stream, kind != 1, kind == 2);
     hipError_t e = hipStreamEndCapture(ctx->stream, &g);
     if (rc) { if (g) hipGraphDestroy(g); return rc; }
     if (e != hipSuccess) return set_err(ctx, XH_E_HIP, "graph capture failed: %s", hipGetErrorString(e));
@@ -532,6 +585,7 @@ int capture(xh_ctx* ctx, int kind, hipGraphExec_t* out) {
 }
 
 int run_step(xh_ctx* ctx, bool with_logits) {
+    if (with_logits) ctx->cand_valid = true;  // the lm_head launch writes candidates
     if (!ctx->use_graphs) return enqueue_step(ctx, ctx->stream, with_logits);
     hipGraphExec_t* ge = with_logits ? &ctx->g_logits : &ctx->g_hydrate;
     if (!*ge) {
@@ -630,6 +684,12 @@ int xh_create(const xh_config* cfg, int device_ordinal, xh_ctx** out) {
     CREATE_TRY(dmalloc(ctx, &ctx->part_ml, (size_t)ctx->nsplit * c.n_heads * 2));
     CREATE_TRY(dmalloc(ctx, &ctx->attn_cnt, (size_t)c.n_kv_heads));
     CREATE_TRY(dmalloc(ctx, &ctx->aw_sync, (size_t)c.n_layers * 4));
+    CREATE_TRY(dmalloc(ctx, &ctx->qaw_sync, qaw_words(c)));
+    CREATE_TRY(dmalloc(ctx, &ctx->cand, (size_t)ARGMAX_CANDS));
+    // fused launch: at most 16 splits per KV head (the attention workgroups stay a small part
+    // of the 2-per-CU grid); partial buffers are sized for ctx->nsplit >= this
+    ctx->qaw_nsplit = std::min(ctx->nsplit, 16);
+    ctx->qaw_t_max = attn_split_len(c.max_seq_len, ctx->qaw_nsplit, attn_min_t(c.head_dim, QAW_THREADS));
     {
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, device_ordinal) != hipSuccess) {
@@ -705,7 +765,7 @@ void xh_destroy(xh_ctx* ctx) {
     if (ctx->wcls && ctx->wcls != ctx->embed) hipFree(ctx->wcls);
     hipFree(ctx->embed); hipFree(ctx->final_norm);
     hipFree(ctx->kv); hipFree(ctx->x); hipFree(ctx->q); hipFree(ctx->attn_out); hipFree(ctx->hb);
-    hipFree(ctx->logits); hipFree(ctx->part_o); hipFree(ctx->part_ml); hipFree(ctx->attn_cnt); hipFree(ctx->aw_sync); hipFree(ctx->rope_freq);
+    hipFree(ctx->logits); hipFree(ctx->part_o); hipFree(ctx->part_ml); hipFree(ctx->attn_cnt); hipFree(ctx->aw_sync); hipFree(ctx->qaw_sync); hipFree(ctx->cand); hipFree(ctx->rope_freq);
     hipFree(ctx->pk_layers); hipFree(ctx->pk_counters); hipFree(ctx->pk_tickets); hipFree(ctx->pk_err);
     hipFree(ctx->pk_cand); hipFree(ctx->pk_prompt); hipFree(ctx->pk_trace);
     if (ctx->pk_host) hipHostFree(ctx->pk_host);
@@ -937,15 +997,19 @@ int xh_decode_greedy(xh_ctx* ctx, int pos, int n_steps, int stop_a, int stop_b, 
         rc = capture(ctx, 2, &ctx->g_decode);
         if (rc) return rc;
     }
+    // the first token is the argmax of the logits on the device: candidates from them if the
+    // launch that produced them left none (persistent engine, or nothing yet)
+    if (!ctx->cand_valid)
+        hipLaunchKernelGGL(logits_cand_kernel, dim3(1), dim3(ARGMAX_CANDS), 0, ctx->stream, (const float*)ctx->logits,
+                           ctx->c.vocab_size, ctx->cand);
+    ctx->cand_valid = true;
     const bool stops = stop_a >= 0 || stop_b >= 0;
     int done = 0;
     for (int i = 0; i < n_steps; i++) {
         if (ctx->use_graphs) {
             HIP_TRY(ctx, hipGraphLaunch(ctx->g_decode, ctx->stream));
         } else {
-            hipLaunchKernelGGL(argmax_advance_kernel, dim3(1), dim3(1024), 0, ctx->stream, (const float*)ctx->logits,
-                               ctx->c.vocab_size, ctx->sp, ctx->dec_tokens, ctx->dec_cap);
-            rc = enqueue_step(ctx, ctx->stream, true);
+            rc = enqueue_step(ctx, ctx->stream, true, true);
             if (rc) return rc;
         }
         done = i + 1;
@@ -980,6 +1044,9 @@ int xh_reset(xh_ctx* ctx) {
     HIP_TRY(ctx, hipMemsetAsync(ctx->kv, 0, (size_t)c.n_layers * 2 * c.max_seq_len * ctx->kv_dim * 2, ctx->stream));
     HIP_TRY(ctx, hipMemsetAsync(ctx->x, 0, (size_t)c.dim * 4, ctx->stream));
     HIP_TRY(ctx, hipMemsetAsync(ctx->logits, 0, (size_t)c.vocab_size * 4, ctx->stream));
+    HIP_TRY(ctx, hipMemsetAsync(ctx->qaw_sync, 0, qaw_words(c) * 4, ctx->stream));
+    HIP_TRY(ctx, hipMemsetAsync(ctx->cand, 0, ARGMAX_CANDS * 8, ctx->stream));
+    ctx->cand_valid = true;  // all-zero candidates = zero logits (argmax token 0)
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     return 0;
 }
@@ -1083,10 +1150,23 @@ int xh_debug_trace(xh_ctx* ctx, int enable, uint64_t* out, int cap, int* len) {
     if (enable >= 0) {
         ctx->pk_trace_on = (enable & 1) != 0;
         ctx->aw_trace_on = (enable & 2) != 0;
+        ctx->qaw_trace_on = (enable & 4) != 0;
         drop_graphs(ctx);
         HIP_TRY(ctx, hipMemset(ctx->pk_trace, 0, (size_t)n * sizeof(uint64_t)));
     }
     return 0;
+}
+
+int xh_get_option(const xh_ctx* ctx, int option, int* value) {
+    if (!ctx || !value) return XH_E_INVALID;
+    switch (option) {
+        case XH_OPT_FUSE_ATTN_WO:
+            // effective level: 2 only while the one-launch form is instantiated for this model
+            *value = ctx->fuse_level >= 2 && ctx->qaw_ok && aw_instantiated(ctx->c.head_dim, ctx->qpk) ? 2
+                     : ctx->fuse_attn_wo ? 1 : 0;
+            return 0;
+        default: return XH_E_INVALID;
+    }
 }
 
 int xh_get_engine(const xh_ctx* ctx) {
@@ -1098,7 +1178,9 @@ int xh_set_option(xh_ctx* ctx, int option, int value) {
     if (!ctx) return XH_E_INVALID;
     switch (option) {
         case XH_OPT_FUSE_ATTN_WO:
+            if (value < 0 || value > 2) return set_err(ctx, XH_E_INVALID, "fuse level %d not in 0..2", value);
             ctx->fuse_attn_wo = value != 0;
+            ctx->fuse_level = value;
             drop_graphs(ctx);
             return 0;
         default: return set_err(ctx, XH_E_INVALID, "unknown option %d", option);
@@ -1225,7 +1307,7 @@ int xh_time_kernel(xh_ctx* ctx, int which, int iters, float* avg_us) {
             case 1: return launch_gemv<PRO_RMSNORM, EPI_QKV>(ctx->L[l].qkv_dt, qkv_args(ctx, l), ctx->stream, mb);
             case 2: return launch_gemv<PRO_PLAIN, EPI_RESID>(ctx->L[l].wo_dt, wo_args(ctx, l), ctx->stream, mb);
             case 3: return launch_gemv<PRO_PLAIN, EPI_RESID>(ctx->L[l].w2_dt, w2_args(ctx, l), ctx->stream, mb);
-            case 4: return launch_gemv<PRO_RMSNORM, EPI_STORE>(ctx->wcls_dt, cls_args(ctx), ctx->stream, mb);
+            case 4: return launch_gemv<PRO_RMSNORM, EPI_LOGITS>(ctx->wcls_dt, cls_args(ctx), ctx->stream, mb);
             default:
                 return launch_attn(attn_args(ctx, l), ctx->c.head_dim, ctx->qpk, ctx->c.n_kv_heads, ctx->t_max,
                                    ctx->stream);

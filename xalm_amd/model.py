@@ -126,6 +126,11 @@ class Model:
     def set_option(self, option: int, value: int):
         L.check(L.lib().xh_set_option(self._ctx, int(option), int(value)), self._ctx)
 
+    def get_option(self, option: int) -> int:
+        v = ctypes.c_int(0)
+        L.check(L.lib().xh_get_option(self._ctx, int(option), ctypes.byref(v)), self._ctx)
+        return int(v.value)
+
     def active_bytes(self, pos: int) -> int:
         return int(L.lib().xh_active_bytes(self._ctx, pos))
 
