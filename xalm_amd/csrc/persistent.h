@@ -103,11 +103,35 @@ __device__ __forceinline__ uint64_t pk_now() { return __builtin_amdgcn_s_memreal
 
 __device__ __forceinline__ unsigned long long pk_key(const float v, const int idx) { return argmax_key(v, idx); }
 
-// publish: every wave's sc1 stores drained, then one add (after a workgroup barrier)
+// Counters are addressed logically (a.counters + k) and stored sharded: counter k occupies
+// PK_SHARDS lines of its own, one per XCD, so 256 arrivals are 8 parallel fan-ins of 32
+// (MI355X_MICROARCH.md "fanin": ~11-13 ns per serialized atomic).
+constexpr int PK_SHARDS = 8;
+constexpr int PK_SHARD_STRIDE = 32;  // uints: one 128-B line per shard
+constexpr int PK_CSLOT = PK_SHARDS * PK_SHARD_STRIDE;
+__device__ __forceinline__ unsigned* pk_shard(const unsigned* c, const int shard) {
+    unsigned* base = pk_args()->counters;
+    return base + (size_t)(c - base) * PK_CSLOT + shard * PK_SHARD_STRIDE;
+}
+__device__ __forceinline__ int pk_xcc() {
+    int v;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 3)" : "=s"(v));
+    return v & (PK_SHARDS - 1);
+}
+
+// publish: every wave's sc1 stores drained, then one add (after a workgroup barrier) on this
+// XCD's shard
 __device__ __forceinline__ void pk_signal(unsigned* c, const unsigned add = 1) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (pk_tid() == 0) __hip_atomic_fetch_add(c, add, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (pk_tid() == 0)
+        __hip_atomic_fetch_add(pk_shard(c, pk_xcc()), add, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned pk_count(const unsigned* c) {
+    unsigned s = 0;
+#pragma unroll
+    for (int k = 0; k < PK_SHARDS; k++) s += __hip_atomic_load(pk_shard(c, k), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return s;
 }
 
 // wait until *c >= target (one lane polls, relaxed, with s_sleep; 2 s bound); false on error
@@ -116,7 +140,7 @@ __device__ __forceinline__ bool pk_wait(const unsigned* c, const unsigned target
         int ok = 1;
         const uint64_t t0 = pk_now();
         unsigned spins = 0;
-        while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+        while (pk_count(c) < target) {
             __builtin_amdgcn_s_sleep(1);
             if ((++spins & 255) == 0) {
                 if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) { ok = 0; break; }
@@ -135,18 +159,50 @@ __device__ __forceinline__ bool pk_wait(const unsigned* c, const unsigned target
     return ok != 0;
 }
 
-// x image for a gemv phase: src (sc1) optionally rms-normalised, permuted as stage_x
-template <int E>
-__device__ __forceinline__ void pk_stage(const float* src, const int n, const void* norm_w, const int norm_dt,
-                                         const float eps, float4* xs4, float* red) {
+// x image for a gemv phase: src (sc1) optionally rms-normalised, permuted as stage_x.  All of
+// a thread's x (and norm) loads are issued before any is used: one memory round trip, not one
+// per float4 (the wave's prefetched weight chunks were issued earlier, so the first use waits
+// for those too).  J = float4 per thread (n <= 4 * J * PK_THREADS).
+template <int E, int J>
+__device__ __forceinline__ void pk_stage_j(const float* src, const int n, const void* norm_w, const int norm_dt,
+                                           const float eps, float4* xs4, float* red) {
     const int tid = pk_tid();
+    const int n4 = n >> 2;
+    u32x4 u[J];
+#pragma unroll
+    for (int j = 0; j < J; j++) u[j] = ld_sc1_x4(src, (uint32_t)min(tid + j * PK_THREADS, n4 - 1) * 16);
+    float4 w[J];
+    if (norm_w) {
+#pragma unroll
+        for (int j = 0; j < J; j++) w[j] = load_norm4_nb(norm_w, norm_dt, n, min(tid + j * PK_THREADS, n4 - 1));
+    }
     float scale = 1.f;
-    // first pass: pull x (sc1, 16 B) into the image and, for rmsnorm, sum squares
-    float ss = 0.f;
-    for (int i = tid; i < (n >> 2); i += PK_THREADS) {
-        const u32x4 u = ld_sc1_x4(src, (uint32_t)i * 16);
-        float4 v = make_float4(bits_f32(u.x), bits_f32(u.y), bits_f32(u.z), bits_f32(u.w));
-        ss += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+    if (norm_w) {
+        float ss = 0.f;
+#pragma unroll
+        for (int j = 0; j < J; j++) {
+            const float d = bits_f32(u[j].x) * bits_f32(u[j].x) + bits_f32(u[j].y) * bits_f32(u[j].y) +
+                            bits_f32(u[j].z) * bits_f32(u[j].z) + bits_f32(u[j].w) * bits_f32(u[j].w);
+            ss += (tid + j * PK_THREADS < n4) ? d : 0.f;
+        }
+        ss = wave_sum(ss);
+        if ((tid & 63) == 0) red[tid >> 6] = ss;
+        __syncthreads();
+        float tot = 0.f;
+#pragma unroll
+        for (int wv = 0; wv < PK_WAVES; wv++) tot += red[wv];
+        scale = 1.0f / sqrtf(tot / (float)n + eps);
+    }
+#pragma unroll
+    for (int j = 0; j < J; j++) {
+        const int i = min(tid + j * PK_THREADS, n4 - 1);  // duplicates store the same value
+        float4 v = make_float4(bits_f32(u[j].x), bits_f32(u[j].y), bits_f32(u[j].z), bits_f32(u[j].w));
+        if (norm_w) {
+            v.x = v.x * scale * w[j].x;
+            v.y = v.y * scale * w[j].y;
+            v.z = v.z * scale * w[j].z;
+            v.w = v.w * scale * w[j].w;
+        }
         const int c = i << 2;
         const int it = c / (64 * E);
         const int rem = c - it * 64 * E;
@@ -154,29 +210,14 @@ __device__ __forceinline__ void pk_stage(const float* src, const int n, const vo
         const int qd = (rem - l * E) >> 2;
         xs4[(it * (E / 4) + qd) * 64 + l] = v;
     }
-    if (norm_w) {
-        ss = wave_sum(ss);
-        if ((tid & 63) == 0) red[tid >> 6] = ss;
-        __syncthreads();
-        float tot = 0.f;
-#pragma unroll
-        for (int w = 0; w < PK_WAVES; w++) tot += red[w];
-        scale = 1.0f / sqrtf(tot / (float)n + eps);
-        for (int i = tid; i < (n >> 2); i += PK_THREADS) {
-            const int c = i << 2;
-            const int it = c / (64 * E);
-            const int rem = c - it * 64 * E;
-            const int l = rem / E;
-            const int qd = (rem - l * E) >> 2;
-            float4& v = xs4[(it * (E / 4) + qd) * 64 + l];
-            const float4 w = load_norm4(norm_w, norm_dt, i);
-            v.x = v.x * scale * w.x;
-            v.y = v.y * scale * w.y;
-            v.z = v.z * scale * w.z;
-            v.w = v.w * scale * w.w;
-        }
-    }
     __syncthreads();
+}
+template <int E>
+__device__ __forceinline__ void pk_stage(const float* src, const int n, const void* norm_w, const int norm_dt,
+                                         const float eps, float4* xs4, float* red) {
+    if ((n >> 2) <= 2 * PK_THREADS) pk_stage_j<E, 2>(src, n, norm_w, norm_dt, eps, xs4, red);
+    else if ((n >> 2) <= 4 * PK_THREADS) pk_stage_j<E, 4>(src, n, norm_w, norm_dt, eps, xs4, red);
+    else pk_stage_j<E, 8>(src, n, norm_w, norm_dt, eps, xs4, red);  // host: n <= 4 * 8 * PK_THREADS
 }
 
 // Per-wave streaming state: the register chunk in flight and which group it belongs to.

@@ -102,7 +102,7 @@ struct xh_ctx {
     int engine = -1;            // -1 auto, 0 graph of kernels, 1 persistent
     int n_cu = 0;
     PkLayer* pk_layers = nullptr;        // device [n_layers]
-    unsigned* pk_counters = nullptr;     // device [n_layers * PK_PHASES + 1]
+    unsigned* pk_counters = nullptr;     // device [n_layers * PK_PHASES + 1][PK_CSLOT] (sharded)
     int* pk_tickets = nullptr;           // device [n_kv_heads]
     int* pk_err = nullptr;               // device [2]: err, n_done
     unsigned long long* pk_cand = nullptr;  // device [n_cu]
@@ -471,6 +471,8 @@ int pk_nsplit(const xh_ctx* ctx) {
 
 // the weight dtypes the persistent kernel is instantiated for, or false
 bool pk_dtypes(const xh_ctx* ctx, int* dt, int* dtc, int* norm_dt) {
+    // pk_stage holds at most 8 float4 of x per thread
+    if (ctx->c.hidden_dim > 32 * PK_THREADS || ctx->c.dim > 32 * PK_THREADS || ctx->q_dim > 32 * PK_THREADS) return false;
     const xh_config& c = ctx->c;
     *dt = ctx->L[0].qkv_dt;
     *norm_dt = ctx->L[0].an_dt;
@@ -524,7 +526,7 @@ int run_persistent(xh_ctx* ctx, const int* prompt, int n_prompt, int n_gen, int 
         HIP_TRY(ctx, hipMemcpyAsync(ctx->pk_prompt, ctx->pk_host + 2, (size_t)n_prompt * sizeof(int),
                                     hipMemcpyHostToDevice, ctx->stream));
     }
-    HIP_TRY(ctx, hipMemsetAsync(ctx->pk_counters, 0, ((size_t)c.n_layers * PK_PHASES + 1) * sizeof(unsigned),
+    HIP_TRY(ctx, hipMemsetAsync(ctx->pk_counters, 0, ((size_t)c.n_layers * PK_PHASES + 1) * PK_CSLOT * sizeof(unsigned),
                                 ctx->stream));
     HIP_TRY(ctx, hipMemsetAsync(ctx->pk_err, 0, 2 * sizeof(int), ctx->stream));
     PkArgs a{};
@@ -701,7 +703,7 @@ int xh_create(const xh_config* cfg, int device_ordinal, xh_ctx** out) {
     }
     ctx->pk_prompt_cap = 1 << 16;
     CREATE_TRY(dmalloc(ctx, &ctx->pk_layers, (size_t)c.n_layers));
-    CREATE_TRY(dmalloc(ctx, &ctx->pk_counters, (size_t)c.n_layers * PK_PHASES + 1));
+    CREATE_TRY(dmalloc(ctx, &ctx->pk_counters, ((size_t)c.n_layers * PK_PHASES + 1) * PK_CSLOT));
     CREATE_TRY(dmalloc(ctx, &ctx->pk_tickets, (size_t)c.n_kv_heads));
     CREATE_TRY(dmalloc(ctx, &ctx->pk_err, 2));
     CREATE_TRY(dmalloc(ctx, &ctx->pk_cand, (size_t)ctx->n_cu));
