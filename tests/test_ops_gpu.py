@@ -109,3 +109,43 @@ def test_mha_peaked_softmax_and_32k():
     got = L.op_mha(kb, vb, q, head_dim, kv_len, msl, n_heads, n_kv)
     cpu = O.mha(kb, vb, q, head_dim, kv_len, msl, n_heads, n_kv)
     assert np.abs(got - cpu).max() < 5e-5, np.abs(got - cpu).max()
+
+
+def _special(codes, dtype):
+    # OCP NaN/Inf patterns, where gfx950's converter and the reference's bit decode differ
+    return (codes & 0x7C) == 0x7C if dtype == L.F8_E5M2 else (codes & 0x7F) == 0x7F
+
+
+@pytest.mark.parametrize("dtype", [L.F8_E4M3, L.F8_E5M2])
+@pytest.mark.parametrize("with_special", [False, True])
+def test_f8_decode_every_code(dtype, with_special):
+    """Every fp8 code through the matvec, bit-exact against the reference decode
+    (src/types.h:302-314).  Without NaN/Inf codes the matrix takes the hardware converter
+    (v_cvt_pk_f32_fp8/_bf8); with them, the exact bit form."""
+    codes = np.arange(256, dtype=np.uint8)
+    if not with_special:
+        codes = codes[~_special(codes, dtype)]
+    d, n = codes.size, 64
+    w = np.zeros((d, n), dtype=np.uint8)
+    w[:, 5] = codes  # one nonzero column: y[r] = decode(code r) * 1.0, exactly
+    x = np.zeros(n, dtype=np.float32)
+    x[5] = 1.0
+    got = L.op_matmul(x, w, dtype, n, d)
+    ref = np.array([O.decode(dtype, codes, i) for i in range(d)], dtype=np.float32)
+    ref = ref + np.float32(0.0)  # the fp32 sum starts at +0: code 0x80 (-0) sums to +0
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+
+
+@pytest.mark.parametrize("dtype", [L.F8_E4M3, L.F8_E5M2])
+@pytest.mark.parametrize("n,d", [(4096, 64), (1536, 96)])
+def test_matmul_f8_hw(dtype, n, d):
+    """Random finite fp8 weights (the converter path) vs the oracle."""
+    rng = np.random.default_rng(n + d + dtype)
+    x = rng.standard_normal(n).astype(np.float32)
+    w = rng.integers(0, 256, size=(d, n), dtype=np.uint8)
+    w[_special(w, dtype)] = 0x01
+    got = L.op_matmul(x, w, dtype, n, d)
+    cpu = O.matmul(x, w, dtype, n, d)
+    wd = decoded(w, dtype).reshape(d, n)
+    mag = np.abs(wd) @ np.abs(x.astype(np.float64))
+    assert np.all(np.abs(got - cpu) <= 2e-6 * mag + 1e-7), np.abs(got - cpu).max()

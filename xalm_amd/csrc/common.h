@@ -6,9 +6,9 @@
 //   e4m3  : ((b&0x80)<<24 | (b&0x7f)<<20) * 2^120        (f8_t::to_float, src/types.h:302-314)
 //   e5m2  : ((b&0x80)<<24 | (b&0x7f)<<21) * 2^112        (same, M=2)
 //   q8    : (1.f/100.f) * (float)int8                    (Type::Q8, src/types.h:423-424)
-// The fp8 forms equal OCP e4m3fn / e5m2 for every finite code and give the reference's
-// finite values for the NaN/Inf codes (e4m3 0x7F -> 480), which the hardware converter
-// would not, so the bit form is used.
+// The fp8 bit forms equal OCP e4m3fn / e5m2 for every finite code and give the reference's
+// finite values for the NaN/Inf codes (e4m3 0x7F -> 480), which the hardware converter would
+// not: matrices use the converter unless they hold such a code (WDec<*_EXACT>).
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -70,7 +70,37 @@ __device__ __forceinline__ void dec_f8_word(const uint32_t w, float* f) {
     }
 }
 
+// fp8 with the gfx950 converter (v_cvt_pk_f32_fp8 / _bf8: OCP e4m3fn / e5m2, 2 elements per
+// instruction).  Equal to the reference's bit form for every code except the NaN/Inf codes
+// (e4m3 0x7F/0xFF; e5m2 exponent 31), which the host detects at upload: a matrix holding
+// any of them is decoded with the *_EXACT forms below instead.
+template <bool BF8>
+__device__ __forceinline__ void dec_f8_hw(const u32x4 v, float* f) {
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const f2_t lo = BF8 ? __builtin_amdgcn_cvt_pk_f32_bf8(w[i], false) : __builtin_amdgcn_cvt_pk_f32_fp8(w[i], false);
+        const f2_t hi = BF8 ? __builtin_amdgcn_cvt_pk_f32_bf8(w[i], true) : __builtin_amdgcn_cvt_pk_f32_fp8(w[i], true);
+        f[4 * i + 0] = lo.x;
+        f[4 * i + 1] = lo.y;
+        f[4 * i + 2] = hi.x;
+        f[4 * i + 3] = hi.y;
+    }
+}
 template <> struct WDec<XH_F8_E4M3> {
+    static constexpr int E = 16;
+    __device__ __forceinline__ static void dec(const u32x4 v, float* f) { dec_f8_hw<false>(v, f); }
+};
+template <> struct WDec<XH_F8_E5M2> {
+    static constexpr int E = 16;
+    __device__ __forceinline__ static void dec(const u32x4 v, float* f) { dec_f8_hw<true>(v, f); }
+};
+
+// internal kernel dtypes: fp8 matrices that hold NaN/Inf codes, decoded bit-exactly as the
+// reference (f8_t::to_float, src/types.h:302-314: finite values for every code)
+constexpr int XH_F8_E4M3_EXACT = 106;
+constexpr int XH_F8_E5M2_EXACT = 107;
+template <> struct WDec<XH_F8_E4M3_EXACT> {
     static constexpr int E = 16;
     __device__ __forceinline__ static void dec(const u32x4 v, float* f) {
         dec_f8_word<20, 120>(v.x, f);
@@ -79,8 +109,7 @@ template <> struct WDec<XH_F8_E4M3> {
         dec_f8_word<20, 120>(v.w, f + 12);
     }
 };
-
-template <> struct WDec<XH_F8_E5M2> {
+template <> struct WDec<XH_F8_E5M2_EXACT> {
     static constexpr int E = 16;
     __device__ __forceinline__ static void dec(const u32x4 v, float* f) {
         dec_f8_word<21, 112>(v.x, f);
@@ -89,6 +118,10 @@ template <> struct WDec<XH_F8_E5M2> {
         dec_f8_word<21, 112>(v.w, f + 12);
     }
 };
+// the code's NaN/Inf pattern under OCP (where the hardware converter and the reference differ)
+__host__ __device__ inline bool f8_special(const uint8_t b, const bool e5m2) {
+    return e5m2 ? (b & 0x7Cu) == 0x7Cu : (b & 0x7Fu) == 0x7Fu;
+}
 
 template <> struct WDec<XH_Q8> {
     static constexpr int E = 16;

@@ -49,6 +49,11 @@ bool matrix_dtype_ok(int dt) {
     return dt == XH_F32 || dt == XH_F16 || dt == XH_BF16 || dt == XH_F8_E4M3 || dt == XH_F8_E5M2 || dt == XH_Q8;
 }
 int elems_per_16b(int dt) { return 16 / (int)dtype_size(dt); }
+// the kernel's decode form for a matrix: fp8 with NaN/Inf codes -> the exact bit decoder
+int kdt(int dt, bool special) {
+    if (!special) return dt;
+    return dt == XH_F8_E4M3 ? XH_F8_E4M3_EXACT : dt == XH_F8_E5M2 ? XH_F8_E5M2_EXACT : dt;
+}
 
 constexpr int ROWS = 2;  // rows per wave (even: rope pairs, gate/up pairs)
 constexpr int UNROLL = 4;
@@ -58,6 +63,8 @@ struct LayerW {
     void* w13 = nullptr; int w13_dt = 0; unsigned w13_have = 0;   // bit0 w1, bit1 w3
     void* wo = nullptr; int wo_dt = 0;
     void* w2 = nullptr; int w2_dt = 0;
+    // fp8 matrices holding NaN/Inf codes (decoded with the exact bit form, no fused kernels)
+    bool qkv_x = false, w13_x = false, wo_x = false, w2_x = false;
     void* attn_norm = nullptr; int an_dt = 0;
     void* ffn_norm = nullptr; int fn_dt = 0;
 };
@@ -72,7 +79,8 @@ struct xh_ctx {
     std::vector<LayerW> L;
     void* embed = nullptr; int embed_dt = 0;
     void* final_norm = nullptr; int final_norm_dt = 0;
-    void* wcls = nullptr; int wcls_dt = 0;
+    void* wcls = nullptr; int wcls_dt = 0; bool wcls_x = false;
+    int* scan_flag = nullptr;  // device word for the fp8 special-code scan
     int q_dim = 0, kv_dim = 0, qpk = 0;
     uint16_t* kv = nullptr;  // [n_layers][2][max_seq_len][kv_dim]
     float *x = nullptr, *q = nullptr, *attn_out = nullptr, *hb = nullptr, *logits = nullptr;
@@ -199,6 +207,8 @@ bool launch_gemv(int dt, const GemvArgs& a, hipStream_t s, int max_blocks) {
         case XH_F8_E4M3: launch_gemv_t<XH_F8_E4M3, PRO, EPI>(a, s, max_blocks); return true;
         case XH_F8_E5M2: launch_gemv_t<XH_F8_E5M2, PRO, EPI>(a, s, max_blocks); return true;
         case XH_Q8: launch_gemv_t<XH_Q8, PRO, EPI>(a, s, max_blocks); return true;
+        case XH_F8_E4M3_EXACT: launch_gemv_t<XH_F8_E4M3_EXACT, PRO, EPI>(a, s, max_blocks); return true;
+        case XH_F8_E5M2_EXACT: launch_gemv_t<XH_F8_E5M2_EXACT, PRO, EPI>(a, s, max_blocks); return true;
         default: return false;
     }
 }
@@ -339,6 +349,7 @@ __global__ void argmax_advance_kernel(const float* logits, int vocab, StepParams
 
 bool use_attn_wo(const xh_ctx* ctx, int l) {
     const int dt = ctx->L[l].wo_dt;
+    if (ctx->L[l].wo_x) return false;  // exact fp8 decode: the separate launches
     return ctx->fuse_attn_wo && aw_instantiated(ctx->c.head_dim, ctx->qpk) &&
            (dt == XH_F32 || dt == XH_F16 || dt == XH_BF16 || dt == XH_F8_E4M3 || dt == XH_F8_E5M2 || dt == XH_Q8);
 }
@@ -364,7 +375,7 @@ int launch_attn_wo(xh_ctx* ctx, int l, hipStream_t s) {
 // qkv + attention + Wo launch of layer l; XH_E_INVALID = shape not instantiated (fall back)
 int launch_qaw(xh_ctx* ctx, int l, hipStream_t s) {
     const LayerW& w = ctx->L[l];
-    if (w.qkv_dt != w.wo_dt) return XH_E_INVALID;
+    if (w.qkv_dt != w.wo_dt || w.qkv_x || w.wo_x) return XH_E_INVALID;
     AttnArgs aa = attn_args(ctx, l);
     aa.nsplit = ctx->qaw_nsplit;
     const GemvArgs qa = qkv_args(ctx, l), wa = wo_args(ctx, l);
@@ -420,7 +431,7 @@ int enqueue_step(xh_ctx* ctx, hipStream_t s, bool with_logits, bool greedy = fal
             if (rc != XH_E_INVALID) return set_err(ctx, rc, "layer %d: qkv + attention + Wo launch failed", l);
             ctx->qaw_ok = false;  // not instantiated / does not fit: the two-launch form from now on
         }
-        if (!launch_gemv<PRO_RMSNORM, EPI_QKV>(w.qkv_dt, qkv_args(ctx, l), s, mb))
+        if (!launch_gemv<PRO_RMSNORM, EPI_QKV>(kdt(w.qkv_dt, w.qkv_x), qkv_args(ctx, l), s, mb))
             return set_err(ctx, XH_E_INVALID, "layer %d: unsupported qkv dtype %d", l, w.qkv_dt);
         if (use_attn_wo(ctx, l)) {
             const int rc = launch_attn_wo(ctx, l, s);
@@ -428,17 +439,17 @@ int enqueue_step(xh_ctx* ctx, hipStream_t s, bool with_logits, bool greedy = fal
         } else {
             if (!launch_attn(attn_args(ctx, l), c.head_dim, ctx->qpk, c.n_kv_heads, ctx->t_max, s))
                 return set_err(ctx, XH_E_INVALID, "unsupported head_dim %d / q-per-kv %d", c.head_dim, ctx->qpk);
-            if (!launch_gemv<PRO_PLAIN, EPI_RESID>(w.wo_dt, wo_args(ctx, l), s, mb))
+            if (!launch_gemv<PRO_PLAIN, EPI_RESID>(kdt(w.wo_dt, w.wo_x), wo_args(ctx, l), s, mb))
                 return set_err(ctx, XH_E_INVALID, "layer %d: unsupported wo dtype", l);
         }
     mlp:
-        if (!launch_gemv<PRO_RMSNORM, EPI_GLU>(w.w13_dt, w13_args(ctx, l), s, mb))
+        if (!launch_gemv<PRO_RMSNORM, EPI_GLU>(kdt(w.w13_dt, w.w13_x), w13_args(ctx, l), s, mb))
             return set_err(ctx, XH_E_INVALID, "layer %d: unsupported w1/w3 dtype", l);
-        if (!launch_gemv<PRO_PLAIN, EPI_RESID>(w.w2_dt, w2_args(ctx, l), s, mb))
+        if (!launch_gemv<PRO_PLAIN, EPI_RESID>(kdt(w.w2_dt, w.w2_x), w2_args(ctx, l), s, mb))
             return set_err(ctx, XH_E_INVALID, "layer %d: unsupported w2 dtype", l);
     }
     if (with_logits) {
-        if (!launch_gemv<PRO_RMSNORM, EPI_LOGITS>(ctx->wcls_dt, cls_args(ctx), s, mb))
+        if (!launch_gemv<PRO_RMSNORM, EPI_LOGITS>(kdt(ctx->wcls_dt, ctx->wcls_x), cls_args(ctx), s, mb))
             return set_err(ctx, XH_E_INVALID, "unsupported wcls dtype");
     }
     HIP_TRY(ctx, hipGetLastError());
@@ -471,6 +482,9 @@ int pk_nsplit(const xh_ctx* ctx) {
 
 // the weight dtypes the persistent kernel is instantiated for, or false
 bool pk_dtypes(const xh_ctx* ctx, int* dt, int* dtc, int* norm_dt) {
+    if (ctx->wcls_x) return false;
+    for (const LayerW& w : ctx->L)
+        if (w.qkv_x || w.w13_x || w.wo_x || w.w2_x) return false;  // exact fp8 decode: graph engine
     // pk_stage holds at most 8 float4 of x per thread
     if (ctx->c.hidden_dim > 32 * PK_THREADS || ctx->c.dim > 32 * PK_THREADS || ctx->q_dim > 32 * PK_THREADS) return false;
     const xh_config& c = ctx->c;
@@ -688,6 +702,7 @@ int xh_create(const xh_config* cfg, int device_ordinal, xh_ctx** out) {
     CREATE_TRY(dmalloc(ctx, &ctx->aw_sync, (size_t)c.n_layers * 4));
     CREATE_TRY(dmalloc(ctx, &ctx->qaw_sync, qaw_words(c)));
     CREATE_TRY(dmalloc(ctx, &ctx->cand, (size_t)ARGMAX_CANDS));
+    CREATE_TRY(dmalloc(ctx, &ctx->scan_flag, (size_t)1));
     // fused launch: at most 16 splits per KV head (the attention workgroups stay a small part
     // of the 2-per-CU grid); partial buffers are sized for ctx->nsplit >= this
     ctx->qaw_nsplit = std::min(ctx->nsplit, 16);
@@ -767,7 +782,7 @@ void xh_destroy(xh_ctx* ctx) {
     if (ctx->wcls && ctx->wcls != ctx->embed) hipFree(ctx->wcls);
     hipFree(ctx->embed); hipFree(ctx->final_norm);
     hipFree(ctx->kv); hipFree(ctx->x); hipFree(ctx->q); hipFree(ctx->attn_out); hipFree(ctx->hb);
-    hipFree(ctx->logits); hipFree(ctx->part_o); hipFree(ctx->part_ml); hipFree(ctx->attn_cnt); hipFree(ctx->aw_sync); hipFree(ctx->qaw_sync); hipFree(ctx->cand); hipFree(ctx->rope_freq);
+    hipFree(ctx->logits); hipFree(ctx->part_o); hipFree(ctx->part_ml); hipFree(ctx->attn_cnt); hipFree(ctx->aw_sync); hipFree(ctx->qaw_sync); hipFree(ctx->cand); hipFree(ctx->scan_flag); hipFree(ctx->rope_freq);
     hipFree(ctx->pk_layers); hipFree(ctx->pk_counters); hipFree(ctx->pk_tickets); hipFree(ctx->pk_err);
     hipFree(ctx->pk_cand); hipFree(ctx->pk_prompt); hipFree(ctx->pk_trace);
     if (ctx->pk_host) hipHostFree(ctx->pk_host);
@@ -815,7 +830,8 @@ int tensor_slot(xh_ctx* ctx, int kind, int layer, int dtype, Slot* out) {
     out->cols = cols;
     out->pitch = rb;
     drop_graphs(ctx);
-    auto plain = [&](void** dst, int* dst_dt) -> int {
+    auto plain = [&](void** dst, int* dst_dt, bool* special = nullptr) -> int {
+        if (special) *special = false;  // a whole-buffer upload: rescanned after the copy
         if (*dst && *dst_dt != dtype) {
             if (*dst == ctx->wcls && *dst != ctx->embed) ctx->wcls = nullptr;
             hipFree(*dst);
@@ -836,14 +852,14 @@ int tensor_slot(xh_ctx* ctx, int kind, int layer, int dtype, Slot* out) {
     if (kind == XH_FINAL_NORM) return plain(&ctx->final_norm, &ctx->final_norm_dt);
     if (kind == XH_WCLS) {
         if (ctx->wcls == ctx->embed) ctx->wcls = nullptr;
-        return plain(&ctx->wcls, &ctx->wcls_dt);
+        return plain(&ctx->wcls, &ctx->wcls_dt, &ctx->wcls_x);
     }
     LayerW& w = ctx->L[layer];
     switch (kind) {
         case XH_ATTN_NORM: return plain(&w.attn_norm, &w.an_dt);
         case XH_FFN_NORM: return plain(&w.ffn_norm, &w.fn_dt);
-        case XH_WO: return plain(&w.wo, &w.wo_dt);
-        case XH_W2: return plain(&w.w2, &w.w2_dt);
+        case XH_WO: return plain(&w.wo, &w.wo_dt, &w.wo_x);
+        case XH_W2: return plain(&w.w2, &w.w2_dt, &w.w2_x);
         case XH_WQ: case XH_WK: case XH_WV: {
             // fused [Wq; Wk; Wv] rows, one dtype
             if (w.wqkv && w.qkv_dt != dtype) {
@@ -851,6 +867,7 @@ int tensor_slot(xh_ctx* ctx, int kind, int layer, int dtype, Slot* out) {
                     return set_err(ctx, XH_E_INVALID, "layer %d: q/k/v must share one dtype", layer);
                 hipFree(w.wqkv); w.wqkv = nullptr; w.qkv_have = 0;
             }
+            if (!(w.qkv_have & ~(1u << (kind - XH_WQ)))) w.qkv_x = false;  // no other part holds codes
             if (!w.wqkv) HIP_TRY(ctx, hipMalloc(&w.wqkv, (size_t)(ctx->q_dim + 2 * ctx->kv_dim) * rb));
             w.qkv_dt = dtype;
             const size_t row0 = kind == XH_WQ ? 0 : kind == XH_WK ? ctx->q_dim : ctx->q_dim + ctx->kv_dim;
@@ -865,6 +882,7 @@ int tensor_slot(xh_ctx* ctx, int kind, int layer, int dtype, Slot* out) {
                 if (w.w13_have & ~bit) return set_err(ctx, XH_E_INVALID, "layer %d: w1/w3 must share one dtype", layer);
                 hipFree(w.w13); w.w13 = nullptr; w.w13_have = 0;
             }
+            if (!(w.w13_have & ~bit)) w.w13_x = false;
             if (!w.w13) HIP_TRY(ctx, hipMalloc(&w.w13, (size_t)2 * c.hidden_dim * rb));
             w.w13_dt = dtype;
             out->base = (char*)w.w13 + (kind == XH_W3 ? rb : 0);
@@ -874,6 +892,39 @@ int tensor_slot(xh_ctx* ctx, int kind, int layer, int dtype, Slot* out) {
         }
     }
     return set_err(ctx, XH_E_INVALID, "unhandled kind");
+}
+
+// any NaN/Inf fp8 code (f8_special) in a [rows][cols] byte matrix of row pitch `pitch`
+__global__ void f8_special_scan_kernel(const uint8_t* base, size_t pitch, size_t rows, size_t cols, int e5m2, int* flag) {
+    int hit = 0;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < rows * cols; i += (size_t)gridDim.x * blockDim.x) {
+        const size_t r = i / cols;
+        hit |= f8_special(base[r * pitch + (i - r * cols)], e5m2 != 0);
+    }
+    if (hit) *flag = 1;
+}
+
+// after an upload into slot s: record whether the fp8 matrix holds NaN/Inf codes
+int scan_f8(xh_ctx* ctx, int kind, int layer, int dtype, const Slot& s) {
+    if (dtype != XH_F8_E4M3 && dtype != XH_F8_E5M2) return 0;
+    if (kind == XH_EMBED || kind == XH_ATTN_NORM || kind == XH_FFN_NORM || kind == XH_FINAL_NORM) return 0;
+    HIP_TRY(ctx, hipMemsetAsync(ctx->scan_flag, 0, sizeof(int), ctx->stream));
+    hipLaunchKernelGGL(f8_special_scan_kernel, dim3(2048), dim3(256), 0, ctx->stream, (const uint8_t*)s.base, s.pitch,
+                       s.rows, s.cols, (int)(dtype == XH_F8_E5M2), ctx->scan_flag);
+    int hit = 0;
+    HIP_TRY(ctx, hipMemcpyAsync(&hit, ctx->scan_flag, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    if (!hit) return 0;
+    drop_graphs(ctx);
+    if (kind == XH_WCLS) { ctx->wcls_x = true; return 0; }
+    LayerW& w = ctx->L[layer];
+    switch (kind) {
+        case XH_WQ: case XH_WK: case XH_WV: w.qkv_x = true; break;
+        case XH_W1: case XH_W3: w.w13_x = true; break;
+        case XH_WO: w.wo_x = true; break;
+        case XH_W2: w.w2_x = true; break;
+    }
+    return 0;
 }
 
 __global__ void synth_fill_kernel(char* base, size_t pitch, size_t rows, size_t cols, int dtype, uint64_t seed,
@@ -918,7 +969,7 @@ int xh_upload(xh_ctx* ctx, int kind, int layer, int dtype, const void* host, siz
     if (rc) return rc;
     HIP_TRY(ctx, hipMemcpy2D(s.base, s.pitch, host, s.cols * dtype_size(dtype), s.cols * dtype_size(dtype), s.rows,
                              hipMemcpyHostToDevice));
-    return 0;
+    return scan_f8(ctx, kind, layer, dtype, s);
 }
 
 int xh_upload_synthetic(xh_ctx* ctx, int kind, int layer, int dtype, uint64_t seed, float mean, float std) {
@@ -932,7 +983,7 @@ int xh_upload_synthetic(xh_ctx* ctx, int kind, int layer, int dtype, uint64_t se
                        seed, mean, std);
     HIP_TRY(ctx, hipGetLastError());
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-    return 0;
+    return scan_f8(ctx, kind, layer, dtype, s);
 }
 
 int xh_kv_fill_synthetic(xh_ctx* ctx, int layer, int which, int slot0, int n_slots, uint64_t seed, float std) {
@@ -1231,7 +1282,10 @@ int xh_op_matmul(float* xout, const float* x, const void* w, int dtype, int n, i
     GemvArgs a{};
     a.w = bw.p; a.row_bytes = (size_t)n * dtype_size(dtype); a.n = n; a.rows = d;
     a.x = (const float*)bx.p; a.out = (float*)bo.p;
-    launch_gemv<PRO_PLAIN, EPI_STORE>(dtype, a, nullptr, 4096);
+    bool special = false;
+    if (dtype == XH_F8_E4M3 || dtype == XH_F8_E5M2)
+        for (size_t i = 0; i < wbytes && !special; i++) special = f8_special(((const uint8_t*)w)[i], dtype == XH_F8_E5M2);
+    launch_gemv<PRO_PLAIN, EPI_STORE>(kdt(dtype, special), a, nullptr, 4096);
     return op_finish(xout, bo, (size_t)d * 4);
 }
 
@@ -1305,11 +1359,11 @@ int xh_time_kernel(xh_ctx* ctx, int which, int iters, float* avg_us) {
     auto launch = [&]() -> bool {
         const int l = rot++ % ctx->c.n_layers;
         switch (which) {
-            case 0: return launch_gemv<PRO_RMSNORM, EPI_GLU>(ctx->L[l].w13_dt, w13_args(ctx, l), ctx->stream, mb);
-            case 1: return launch_gemv<PRO_RMSNORM, EPI_QKV>(ctx->L[l].qkv_dt, qkv_args(ctx, l), ctx->stream, mb);
-            case 2: return launch_gemv<PRO_PLAIN, EPI_RESID>(ctx->L[l].wo_dt, wo_args(ctx, l), ctx->stream, mb);
-            case 3: return launch_gemv<PRO_PLAIN, EPI_RESID>(ctx->L[l].w2_dt, w2_args(ctx, l), ctx->stream, mb);
-            case 4: return launch_gemv<PRO_RMSNORM, EPI_LOGITS>(ctx->wcls_dt, cls_args(ctx), ctx->stream, mb);
+            case 0: return launch_gemv<PRO_RMSNORM, EPI_GLU>(kdt(ctx->L[l].w13_dt, ctx->L[l].w13_x), w13_args(ctx, l), ctx->stream, mb);
+            case 1: return launch_gemv<PRO_RMSNORM, EPI_QKV>(kdt(ctx->L[l].qkv_dt, ctx->L[l].qkv_x), qkv_args(ctx, l), ctx->stream, mb);
+            case 2: return launch_gemv<PRO_PLAIN, EPI_RESID>(kdt(ctx->L[l].wo_dt, ctx->L[l].wo_x), wo_args(ctx, l), ctx->stream, mb);
+            case 3: return launch_gemv<PRO_PLAIN, EPI_RESID>(kdt(ctx->L[l].w2_dt, ctx->L[l].w2_x), w2_args(ctx, l), ctx->stream, mb);
+            case 4: return launch_gemv<PRO_RMSNORM, EPI_LOGITS>(kdt(ctx->wcls_dt, ctx->wcls_x), cls_args(ctx), ctx->stream, mb);
             default:
                 return launch_attn(attn_args(ctx, l), ctx->c.head_dim, ctx->qpk, ctx->c.n_kv_heads, ctx->t_max,
                                    ctx->stream);
