@@ -252,3 +252,39 @@ def test_multi_split_attention_in_model(engine):
     for i, t in enumerate(nxt):
         om.forward(t, len(toks) + i)
     assert np.abs(st.logits() - om.logits()).max() <= tol(om.logits())
+
+
+@pytest.mark.parametrize("engine", ENGINES)
+@pytest.mark.parametrize("history", [20000, 32767])
+def test_long_context_streaming_attention(engine, history):
+    """Synthetic GQA model (8 KV heads x head_dim 128, 4 q per KV, -T 32768) with a filled KV
+    history: splits longer than one prefetch round take the streaming online-softmax form
+    (attention.h attn_block_stream) inside the fused attention + Wo launch.  One forward at
+    pos = history vs the oracle on the same weights and the same KV rows."""
+    import bench
+
+    if engine == "persistent":
+        pytest.skip("the persistent engine's attention tiles do not fit a 32k split (graph engine only)")
+    w = dict(dim=512, hidden=512, layers=2, heads=32, kv_heads=8, head_dim=128, vocab=256, msl=32768, theta=1e6,
+             wdt=L.F16, edt=L.F16, cdt=L.F16)
+    c = bench.make_config(w)
+    gm = Model(c)
+    configure(gm, engine)
+    om = O.OracleModel(c)
+    for kind, layer, dt, seed, mean, std in bench.tensor_specs(w):
+        gm.upload_synthetic(kind, layer, dt, seed, mean, std)
+        rows, cols = bench.tensor_shape(c, kind)
+        om.set_tensor(kind, layer, dt, O.synthetic(rows, cols, dt, seed, mean, std))
+    kv_dim = c.n_kv_heads * c.head_dim
+    for layer in range(c.n_layers):
+        for which in (0, 1):
+            seed = 700 + 2 * layer + which
+            gm.kv_fill_synthetic(layer, which, 0, history, seed, 1.0)
+            om.set_kv(layer, which, 0, O.synthetic(history, kv_dim, L.F16, seed, 0.0, 1.0))
+    st = InferenceState(c)
+    gm.forward(st, 17, history, L.OUTPUT_LOGITS)
+    om.forward(17, history, L.OUTPUT_LOGITS)
+    ref = om.logits()
+    assert np.abs(st.logits() - ref).max() <= tol(ref)
+    gm.close()
+    om.close()

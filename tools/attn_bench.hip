@@ -1,0 +1,103 @@
+// attn_bench.hip — long-context attention variants, one process (Mistral-7B shapes: 8 KV heads,
+// 4 q per KV, head_dim 128, fp16 ring).  Times the split (partials) phase alone:
+//   round  : attn_block<PARTIALS>  (score pass + softmax + p.V pass, 256-row rounds)
+//   merged : attn_block<SIGNAL>    (the last split of each head merges, attn_wo long contexts)
+// Build: hipcc -O3 --offload-arch=gfx950 -std=c++17 -o tools/attn_bench tools/attn_bench.hip
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <vector>
+
+#include "../include/xalm_synth.h"
+#include "../xalm_amd/csrc/attention.h"
+
+using namespace xalm;
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s @%d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
+
+constexpr int HD = 128, QPK = 4, NKV = 8, NH = 32, KVD = NKV * HD;
+
+__global__ void fill16(uint16_t* p, size_t n, uint64_t seed) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+        p[i] = xs_to_f16(xs_value(seed, i, 0.f, 1.f));
+}
+__global__ void fillf(float* p, size_t n, uint64_t seed) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+        p[i] = xs_value(seed, i, 0.f, 1.f);
+}
+
+template <int THREADS>
+__global__ __launch_bounds__(THREADS) void k_round(const AttnArgs a, unsigned* done) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    attn_block<HD, QPK, THREADS, true>(a, blockIdx.x / a.nsplit, blockIdx.x % a.nsplit, smem, done);
+}
+template <int THREADS>
+__global__ __launch_bounds__(THREADS) void k_signal(const AttnArgs a, unsigned* done) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    attn_block<HD, QPK, THREADS, false, false, attn_min_t_partials(HD, THREADS), NoWait, AddArrive, true>(
+        a, blockIdx.x / a.nsplit, blockIdx.x % a.nsplit, smem, done);
+}
+
+int main(int argc, char** argv) {
+    const int msl = 32768;
+    const int kv_len = argc > 1 ? atoi(argv[1]) : 32768;
+    const int NC = 4;  // ring copies (4 x 128 MB) so the Infinity Cache serves nothing
+    std::vector<uint16_t*> kc(NC), vc(NC);
+    for (int c = 0; c < NC; c++) {
+        CK(hipMalloc(&kc[c], (size_t)msl * KVD * 2));
+        CK(hipMalloc(&vc[c], (size_t)msl * KVD * 2));
+        hipLaunchKernelGGL(fill16, dim3(2048), dim3(256), 0, 0, kc[c], (size_t)msl * KVD, 10 + c);
+        hipLaunchKernelGGL(fill16, dim3(2048), dim3(256), 0, 0, vc[c], (size_t)msl * KVD, 20 + c);
+    }
+    float *q, *po, *pml, *out;
+    int* cnt;
+    CK(hipMalloc(&out, NH * HD * 4));
+    CK(hipMalloc(&cnt, 64));
+    CK(hipMemset(cnt, 0, 64));
+    unsigned* done;
+    StepParams* sp;
+    CK(hipMalloc(&q, NH * HD * 4));
+    CK(hipMalloc(&po, (size_t)128 * NH * HD * 4));
+    CK(hipMalloc(&pml, (size_t)128 * NH * 2 * 4));
+    CK(hipMalloc(&done, 4));
+    CK(hipMalloc(&sp, sizeof(StepParams)));
+    hipLaunchKernelGGL(fillf, dim3(16), dim3(256), 0, 0, q, NH * HD, 3);
+    StepParams h{};
+    h.kv_len = kv_len; h.pos = kv_len - 1; h.kv_pos = kv_len - 1; h.max_seq_len = msl;
+    CK(hipMemcpy(sp, &h, sizeof h, hipMemcpyHostToDevice));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    auto run = [&](auto kern, int threads, int nsplit, size_t smem, const char* name) {
+        CK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        AttnArgs a{};
+        a.q = q; a.kv_dim = KVD; a.n_heads = NH; a.nsplit = nsplit; a.part_o = po; a.part_ml = pml; a.sp = sp; a.out = out; a.counters = cnt;
+        std::vector<float> ts;
+        for (int r = 0; r < 3; r++) {
+            const int it = 20;
+            CK(hipEventRecord(e0, 0));
+            for (int i = 0; i < it; i++) {
+                a.kc = kc[i % NC]; a.vc = vc[i % NC];
+                hipLaunchKernelGGL(kern, dim3(NKV * nsplit), dim3(threads), smem, 0, a, done);
+            }
+            CK(hipEventRecord(e1, 0));
+            CK(hipEventSynchronize(e1));
+            float ms;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            ts.push_back(ms * 1000 / it);
+        }
+        std::sort(ts.begin(), ts.end());
+        const double bytes = 2.0 * kv_len * KVD * 2;
+        printf("  %-22s nsplit %3d  %8.2f us  %7.1f GB/s\n", name, nsplit, ts[1], bytes / (ts[1] * 1e-6) / 1e9);
+    };
+    printf("kv_len %d (%.1f MB of K+V)\n", kv_len, 2.0 * kv_len * KVD * 2 / 1e6);
+    for (int ns : {32, 64, 128}) {
+        const int T = attn_split_len(kv_len, ns, attn_min_t_partials(HD, 1024));
+        run(k_round<1024>, 1024, ns, attn_smem_bytes(HD, QPK, T, ns, 1024), "round   t1024");
+        run(k_signal<1024>, 1024, ns, attn_smem_bytes(HD, QPK, T, ns, 1024), "merged  t1024");
+        const int T5 = attn_split_len(kv_len, ns, attn_min_t_partials(HD, 512));
+        run(k_round<512>, 512, ns, attn_smem_bytes(HD, QPK, T5, ns, 512), "round   t512");
+        run(k_signal<512>, 512, ns, attn_smem_bytes(HD, QPK, T5, ns, 512), "merged  t512");
+    }
+    return 0;
+}

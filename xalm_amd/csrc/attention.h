@@ -81,8 +81,12 @@ struct AddArrive {
 // are read after the hand-off with sc1 loads only, so no stale copy of them can sit in this
 // CU's caches (MI355X_MICROARCH.md "Valid forms", consumer condition 1).
 // MINT: split floor (0 = the default of the mode); `arrive(done)` runs on thread 0.
+// SIGNAL (with !PARTIALS, attn_wo.h long contexts): the block that completes a KV head (its only
+// split, or the last split to arrive, which merges) stores the head's output write-through,
+// drains and calls arrive(done): the consumer waits for n_kv_heads arrivals and reads the
+// merged output, instead of merging n_active partials itself.
 template <int HD, int QPK, int THREADS, bool PARTIALS, bool FUSED = false, int MINT = 0, class Wait = NoWait,
-          class Arrive = AddArrive>
+          class Arrive = AddArrive, bool SIGNAL = false>
 __device__ __forceinline__ void attn_block(const AttnArgs& a, const int g, const int s, char* smem, unsigned* done,
                                            unsigned long long* dbg = nullptr, const Wait& wait = Wait(),
                                            const Arrive& arrive = Arrive()) {
@@ -303,8 +307,19 @@ __device__ __forceinline__ void attn_block(const AttnArgs& a, const int g, const
         if (tid == 0) arrive(done);
         return;
     }
+    auto out_st = [&](const int idx, const float v) {
+        if (SIGNAL) st_sc1(a.out + (size_t)g * NO + idx, v);
+        else a.out[(size_t)g * NO + idx] = v;
+    };
+    auto head_done = [&]() {
+        if (!SIGNAL) return;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) arrive(done);
+    };
     if (n_active == 1) {
-        for (int idx = tid; idx < NO; idx += THREADS) a.out[(size_t)g * NO + idx] = block_sum(idx) / ml[2 * (idx / HD) + 1];
+        for (int idx = tid; idx < NO; idx += THREADS) out_st(idx, block_sum(idx) / ml[2 * (idx / HD) + 1]);
+        head_done();
         return;
     }
 
@@ -355,6 +370,14 @@ __device__ __forceinline__ void attn_block(const AttnArgs& a, const int g, const
         const size_t stride = (size_t)a.n_heads * HD;
         float num = 0.f;
         int j = 0;
+        // 16 partials per round trip (same left-to-right summation order)
+        for (; j + 16 <= n_active; j += 16) {
+            float pv[16];
+#pragma unroll
+            for (int k = 0; k < 16; k++) pv[k] = ld_sc1(src + (j + k) * stride);
+#pragma unroll
+            for (int k = 0; k < 16; k++) num = fmaf(w[j + k], pv[k], num);
+        }
         for (; j + 4 <= n_active; j += 4) {
             const float p0 = ld_sc1(src + (j + 0) * stride), p1 = ld_sc1(src + (j + 1) * stride);
             const float p2 = ld_sc1(src + (j + 2) * stride), p3 = ld_sc1(src + (j + 3) * stride);
@@ -364,8 +387,9 @@ __device__ __forceinline__ void attn_block(const AttnArgs& a, const int g, const
             num = fmaf(w[j + 3], p3, num);
         }
         for (; j < n_active; j++) num = fmaf(w[j], ld_sc1(src + j * stride), num);
-        a.out[(size_t)g * NO + idx] = num / red[h];
+        out_st(idx, num / red[h]);
     }
+    head_done();
 }
 
 #undef ATTN_STAMP

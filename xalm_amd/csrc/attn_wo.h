@@ -34,6 +34,17 @@ template <int DT>
 using AwShape = GemvShape<AW_THREADS, 2, (WDec<DT>::E >= 16 ? 4 : 8), true, 4, true>;
 
 // sync: [0] heads done, [1] Wo workgroups done, [2] timeout flag (sticky, host-checked)
+
+// More than MAXS partials per head to merge (aw_stage_merged keeps MAXS in registers beside
+// the Wo rows): the attention side merges instead (attn_block SIGNAL), so a Wo workgroup
+// reads one merged vector, not n_active partials per element.
+constexpr int AW_MAXS = 4;
+template <int HD>
+__device__ __forceinline__ bool aw_long(const AttnArgs& aa) {
+    const int kv_len = aa.sp->kv_len;
+    const int T = attn_split_len(kv_len, aa.nsplit, attn_min_t_partials(HD, AW_THREADS));
+    return (kv_len + T - 1) / T > AW_MAXS;
+}
 template <int E>
 __host__ __device__ constexpr size_t aw_image_bytes(const int n) {
     return (size_t)((n + 64 * E - 1) / (64 * E)) * 64 * E * sizeof(float);
@@ -45,7 +56,7 @@ __host__ __device__ constexpr size_t aw_image_bytes(const int n) {
 template <int E, int HD, int THREADS = AW_THREADS>
 __device__ __forceinline__ void aw_stage_merged(const AttnArgs& aa, const int n, const int n_active, float4* xs4,
                                                 float* wts) {
-    constexpr int MAXS = 4;  // prefetched partials per thread (registers beside the Wo rows)
+    constexpr int MAXS = AW_MAXS;  // prefetched partials per thread (registers beside the Wo rows)
     const int tid = threadIdx.x;
     const int nh = aa.n_heads;
     const int n4 = n >> 2;
@@ -106,6 +117,20 @@ __device__ __forceinline__ void aw_stage_merged(const AttnArgs& aa, const int n,
     }
 }
 
+// x image of the Wo rows from the merged attention output (sc1: written in this launch)
+template <int E>
+__device__ __forceinline__ void aw_stage_out(const float* src, const int n, float4* xs4) {
+    for (int i = threadIdx.x; i < (n >> 2); i += AW_THREADS) {
+        const u32x4 u = ld_sc1_x4(src, (uint32_t)i * 16);
+        const int c = i << 2;
+        const int it = c / (64 * E);
+        const int rem = c - it * 64 * E;
+        const int l = rem / E;
+        const int qd = (rem - l * E) >> 2;
+        xs4[(it * (E / 4) + qd) * 64 + l] = make_float4(bits_f32(u.x), bits_f32(u.y), bits_f32(u.z), bits_f32(u.w));
+    }
+}
+
 // trace (debug, null = off): per workgroup [8]: start, attention done | hand-off passed, end;
 // attention workgroups also [2] split known, [3] scores done, [4] p.V done, [5] partial drained
 template <int DT, int HD, int QPK>
@@ -119,8 +144,14 @@ __global__ __launch_bounds__(AW_THREADS) void attn_wo_kernel(const AttnArgs aa, 
     const int b = blockIdx.x;
     if (trace && threadIdx.x == 0) trace[8 * b] = __builtin_amdgcn_s_memrealtime();
     if (b < n_att) {
-        attn_block<HD, QPK, AW_THREADS, true>(aa, b / aa.nsplit, b - (b / aa.nsplit) * aa.nsplit, smem, sync,
-                                              trace ? trace + 8 * b : nullptr);
+        const int g = b / aa.nsplit, s = b - g * aa.nsplit;
+        if (aw_long<HD>(aa)) {
+            // long contexts: each KV head's last split merges (ticket) and signals the head
+            attn_block<HD, QPK, AW_THREADS, false, false, attn_min_t_partials(HD, AW_THREADS), NoWait, AddArrive, true>(
+                aa, g, s, smem, sync);
+        } else {
+            attn_block<HD, QPK, AW_THREADS, true>(aa, g, s, smem, sync, trace ? trace + 8 * b : nullptr);
+        }
         if (trace && threadIdx.x == 0) trace[8 * b + 1] = __builtin_amdgcn_s_memrealtime();
         return;
     }
@@ -133,9 +164,10 @@ __global__ __launch_bounds__(AW_THREADS) void attn_wo_kernel(const AttnArgs aa, 
         const int kv_len = aa.sp->kv_len;
         const int T = attn_split_len(kv_len, aa.nsplit, attn_min_t_partials(HD, AW_THREADS));
         const int n_active = (kv_len + T - 1) / T;
+        const bool merged = aw_long<HD>(aa);  // heads arrive merged (one arrival per KV head)
         if (threadIdx.x == 0) {
             const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-            const unsigned target = (unsigned)(n_kv_heads * n_active);
+            const unsigned target = (unsigned)(merged ? n_kv_heads : n_kv_heads * n_active);
             while (__hip_atomic_load(sync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
                 __builtin_amdgcn_s_sleep(1);
                 if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {  // 2 s at 100 MHz: flag, go on
@@ -146,7 +178,8 @@ __global__ __launch_bounds__(AW_THREADS) void attn_wo_kernel(const AttnArgs aa, 
         }
         __syncthreads();
         if (trace && threadIdx.x == 0) trace[8 * b + 1] = __builtin_amdgcn_s_memrealtime();
-        aw_stage_merged<E, HD>(aa, ga.n, n_active, xs4, (float*)(smem + LDS_HEAD_BYTES + aw_image_bytes<E>(ga.n)));
+        if (merged) aw_stage_out<E>(aa.out, ga.n, xs4);
+        else aw_stage_merged<E, HD>(aa, ga.n, n_active, xs4, (float*)(smem + LDS_HEAD_BYTES + aw_image_bytes<E>(ga.n)));
         __syncthreads();
         if (trace && threadIdx.x == 0) trace[8 * b + 3] = __builtin_amdgcn_s_memrealtime();
     };

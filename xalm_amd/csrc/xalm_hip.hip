@@ -255,7 +255,9 @@ bool launch_attn(const AttnArgs& a, int hd, int qpk, int n_kv_heads, int t_max, 
 }
 
 int attn_nsplit(int n_kv_heads, int max_seq_len) {
-    int ns = 512 / n_kv_heads;
+    // one split workgroup per CU at the longest context (tools/attn_bench.hip, 32k: 32 splits
+    // per KV head 34.9 us vs 64 splits 39.0 us)
+    int ns = 256 / n_kv_heads;
     if (ns > 128) ns = 128;  // the merge holds <= 2 partials per lane
     const int cap = (max_seq_len + ATTN_MIN_T - 1) / ATTN_MIN_T;
     if (ns > cap) ns = cap;
