@@ -54,11 +54,19 @@ static int seq_launch1(GemvArgs a, hipStream_t s, unsigned long long* tr) {
     return blocks;
 }
 static int g_seq_pf = 0;
+// 0 plain; 1 PF U4 (product); 2 PF U8 for n=4096 row counts <= 8192 (qkv, wo); 3 PF U8 for
+// n=14336 (w2); 4 = 2 + 3; 5 PF U4 ROWS 1 for w2
 template <int PRO, int EPI>
 static int seq_launch(GemvArgs a, hipStream_t s, unsigned long long* tr = nullptr) {
-    if (!g_seq_pf) return seq_launch1<PRO, EPI, SeqS>(a, s, tr);
-    if (a.n <= 4096) return seq_launch1<PRO, EPI, GemvShape<512, 2, 4, true, 4, true, 2>>(a, s, tr);
-    return seq_launch1<PRO, EPI, GemvShape<512, 2, 4, true, 4, true, 7>>(a, s, tr);
+    const int v = g_seq_pf;
+    if (!v) return seq_launch1<PRO, EPI, SeqS>(a, s, tr);
+    if (a.n <= 4096) {
+        if ((v == 2 || v == 4) && a.rows <= 8192) return seq_launch1<PRO, EPI, GemvShape<512, 2, 8, true, 4, true, 2>>(a, s, tr);
+        return seq_launch1<PRO, EPI, GemvShape<512, 2, 4, true, 4, true, 2>>(a, s, tr);
+    }
+    if (v == 3 || v == 4) return seq_launch1<PRO, EPI, GemvShape<512, 2, 8, true, 4, true, 8>>(a, s, tr);
+    if (v == 5) return seq_launch1<PRO, EPI, GemvShape<512, 1, 4, true, 4, true, 8>>(a, s, tr);
+    return seq_launch1<PRO, EPI, GemvShape<512, 2, 4, true, 4, true, 8>>(a, s, tr);
 }
 
 template <int PRO, int EPI, int U>
@@ -74,6 +82,7 @@ static int chain_launch(const GemvArgs& a, hipStream_t s, const ChainSync& sy, i
 }
 
 int main(int argc, char** argv) {
+    setvbuf(stdout, nullptr, _IONBF, 0);
     const int reps = argc > 1 ? atoi(argv[1]) : 5;
     std::vector<Layer> L(NCOPY);
     for (int c = 0; c < NCOPY; c++) {
@@ -203,15 +212,43 @@ int main(int argc, char** argv) {
         if (ev) return 2;
     }
     std::vector<float> ts, tsp, tc4, tc8, tc1;
+    std::vector<std::vector<float>> tv(6);
     for (int r = 0; r < reps; r++) {
         ts.push_back(run_seq());
-        g_seq_pf = 1;
-        tsp.push_back(run_seq());
+        for (int v = 1; v <= 5; v++) {
+            g_seq_pf = v;
+            tv[v].push_back(run_seq());
+        }
         g_seq_pf = 0;
-        tc4.push_back(run_chain(0));
-        tc8.push_back(run_chain(1));
-        tc1.push_back(run_chain(2));
+        tsp = tv[1];
     }
+    // per-kernel means from a traced run of each variant
+    auto kstats = [&](int v) {
+        const size_t STR = (size_t)NK * 1024 * 4;
+        unsigned long long* tb;
+        CK(hipMalloc(&tb, STR * 8));
+        CK(hipMemset(tb, 0, STR * 8));
+        strace = tb;
+        g_seq_pf = v;
+        run_seq();
+        g_seq_pf = 0;
+        strace = nullptr;
+        std::vector<unsigned long long> hq(STR);
+        CK(hipMemcpy(hq.data(), tb, STR * 8, hipMemcpyDeviceToHost));
+        CK(hipFree(tb));
+        double sum[4] = {0, 0, 0, 0};
+        int cnt[4] = {0, 0, 0, 0};
+        for (int kk = 4; kk < NK; kk++) {  // skip layer 0
+            unsigned long long smin = ~0ull, dmax = 0;
+            const unsigned long long* T = hq.data() + (size_t)kk * 1024 * 4;
+            for (int b = 0; b < sblocks[kk]; b++) { smin = std::min(smin, T[4 * b]); dmax = std::max(dmax, T[4 * b + 2]); }
+            sum[kk % 4] += (dmax - smin) / 100.0;
+            cnt[kk % 4]++;
+        }
+        printf("  variant %d: qkv %6.2f  wo %6.2f  w13 %6.2f  w2 %6.2f us (first start -> last done)\n", v,
+               sum[0] / cnt[0], sum[1] / cnt[1], sum[2] / cnt[2], sum[3] / cnt[3]);
+    };
+    for (int v = 1; v <= 5; v++) kstats(v);
     // timeline of one traced chain run (u4, two streams): per kernel, block start min/max,
     // staged max, done max, signalled max (us from the first kernel's first start)
     tracing = true;
@@ -266,7 +303,13 @@ int main(int argc, char** argv) {
     const double bytes = ((double)QKV * DIM + DIM * DIM + 2.0 * HID * DIM + (double)DIM * HID) * 2;
     printf("per layer (%.1f MB of weights):\n", bytes / 1e6);
     printf("  seq      %8.2f us  %7.1f GB/s\n", med(ts), bytes / (med(ts) * 1e-6) / 1e9);
-    printf("  seq pf   %8.2f us  %7.1f GB/s\n", med(tsp), bytes / (med(tsp) * 1e-6) / 1e9);
+    for (int v = 1; v <= 5; v++)
+        printf("  seq v%d   %8.2f us  %7.1f GB/s\n", v, med(tv[v]), bytes / (med(tv[v]) * 1e-6) / 1e9);
+    for (int r = 0; r < reps; r++) {
+        tc4.push_back(run_chain(0));
+        tc8.push_back(run_chain(1));
+        tc1.push_back(run_chain(2));
+    }
     printf("  chain u4 %8.2f us  %7.1f GB/s\n", med(tc4), bytes / (med(tc4) * 1e-6) / 1e9);
     printf("  chain u8 %8.2f us  %7.1f GB/s\n", med(tc8), bytes / (med(tc8) * 1e-6) / 1e9);
     printf("  chain 1s %8.2f us  %7.1f GB/s (one stream)\n", med(tc1), bytes / (med(tc1) * 1e-6) / 1e9);

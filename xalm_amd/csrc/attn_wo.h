@@ -33,7 +33,12 @@ constexpr int AW_THREADS = AW_THREADS_OVERRIDE;
 template <int DT>
 using AwShape = GemvShape<AW_THREADS, 2, (WDec<DT>::E >= 16 ? 4 : 8), true, 4, true>;
 
-// sync: [0] heads done, [1] Wo workgroups done, [2] timeout flag (sticky, host-checked)
+// sync (AW_SYNC_WORDS per layer): [0] head arrivals, [1] Wo workgroups done, [2] timeout flag
+// (sticky, host-checked), [AW_FLAG0 + 32 k] "heads done" flag of XCD k: set by the last head
+// arrival, polled by that XCD's Wo workgroups (one polled line per XCD instead of every Wo
+// workgroup polling the counter the arrivals add to), reset with [0] by the last Wo workgroup
+constexpr int AW_FLAG0 = 32;
+constexpr int AW_SYNC_WORDS = AW_FLAG0 + 8 * 32;
 
 // More than MAXS partials per head to merge (aw_stage_merged keeps MAXS in registers beside
 // the Wo rows): the attention side merges instead (attn_block SIGNAL), so a Wo workgroup
@@ -143,14 +148,28 @@ __global__ __launch_bounds__(AW_THREADS) void attn_wo_kernel(const AttnArgs aa, 
     const int n_att = n_kv_heads * aa.nsplit;
     const int b = blockIdx.x;
     if (trace && threadIdx.x == 0) trace[8 * b] = __builtin_amdgcn_s_memrealtime();
+    const int kv_len = aa.sp->kv_len;
+    const int T = attn_split_len(kv_len, aa.nsplit, attn_min_t_partials(HD, AW_THREADS));
+    const int n_active = (kv_len + T - 1) / T;
+    const bool merged = aw_long<HD>(aa);  // heads arrive merged (one arrival per KV head)
+    const unsigned target = (unsigned)(merged ? n_kv_heads : n_kv_heads * n_active);
     if (b < n_att) {
         const int g = b / aa.nsplit, s = b - g * aa.nsplit;
-        if (aw_long<HD>(aa)) {
+        auto arrive = [&](unsigned* c) {
+            const unsigned old = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (old + 1 == target) {
+#pragma unroll
+                for (int k = 0; k < 8; k++)
+                    __hip_atomic_store(c + AW_FLAG0 + 32 * k, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        };
+        if (merged) {
             // long contexts: each KV head's last split merges (ticket) and signals the head
-            attn_block<HD, QPK, AW_THREADS, false, false, attn_min_t_partials(HD, AW_THREADS), NoWait, AddArrive, true>(
-                aa, g, s, smem, sync);
+            attn_block<HD, QPK, AW_THREADS, false, false, attn_min_t_partials(HD, AW_THREADS), NoWait,
+                       decltype(arrive), true>(aa, g, s, smem, sync, nullptr, NoWait(), arrive);
         } else {
-            attn_block<HD, QPK, AW_THREADS, true>(aa, g, s, smem, sync, trace ? trace + 8 * b : nullptr);
+            attn_block<HD, QPK, AW_THREADS, true, false, 0, NoWait, decltype(arrive)>(
+                aa, g, s, smem, sync, trace ? trace + 8 * b : nullptr, NoWait(), arrive);
         }
         if (trace && threadIdx.x == 0) trace[8 * b + 1] = __builtin_amdgcn_s_memrealtime();
         return;
@@ -161,14 +180,12 @@ __global__ __launch_bounds__(AW_THREADS) void attn_wo_kernel(const AttnArgs aa, 
     const int nb = gridDim.x - n_att;
     const int g = (b - n_att) * S::WAVES + wid;
     auto wait_heads = [&]() {
-        const int kv_len = aa.sp->kv_len;
-        const int T = attn_split_len(kv_len, aa.nsplit, attn_min_t_partials(HD, AW_THREADS));
-        const int n_active = (kv_len + T - 1) / T;
-        const bool merged = aw_long<HD>(aa);  // heads arrive merged (one arrival per KV head)
         if (threadIdx.x == 0) {
             const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-            const unsigned target = (unsigned)(merged ? n_kv_heads : n_kv_heads * n_active);
-            while (__hip_atomic_load(sync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+            int xcc;
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 3)" : "=s"(xcc));
+            const unsigned* flag = sync + AW_FLAG0 + 32 * (xcc & 7);
+            while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
                 __builtin_amdgcn_s_sleep(1);
                 if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {  // 2 s at 100 MHz: flag, go on
                     __hip_atomic_store(sync + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -228,6 +245,8 @@ __global__ __launch_bounds__(AW_THREADS) void attn_wo_kernel(const AttnArgs aa, 
         if (c == (unsigned)nb - 1) {
             __hip_atomic_store(sync, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(sync + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+            for (int k = 0; k < 8; k++) __hip_atomic_store(sync + AW_FLAG0 + 32 * k, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
 }

@@ -360,7 +360,7 @@ int launch_attn_wo(xh_ctx* ctx, int l, hipStream_t s) {
     const AttnArgs aa = attn_args(ctx, l);
     GemvArgs ga = wo_args(ctx, l);
     if (getenv("XH_AW_NOPF")) ga.act |= 256;  // experiment: Wo loads after the hand-off
-    unsigned* sync = ctx->aw_sync + 4 * l;
+    unsigned* sync = ctx->aw_sync + (size_t)AW_SYNC_WORDS * l;
     const int hd = ctx->c.head_dim, qpk = ctx->qpk, nkv = ctx->c.n_kv_heads, tm = ctx->t_max_aw;
     const int mw = ctx->max_gemv_waves;
     switch (ctx->L[l].wo_dt) {
@@ -407,10 +407,10 @@ int check_aw(xh_ctx* ctx) {
         if (e) return set_err(ctx, XH_E_HIP, "qkv -> attention -> Wo hand-off timed out");
     }
     if (!ctx->fuse_attn_wo) return 0;
-    std::vector<unsigned> h((size_t)ctx->c.n_layers * 4);
+    std::vector<unsigned> h((size_t)ctx->c.n_layers * AW_SYNC_WORDS);
     HIP_TRY(ctx, hipMemcpy(h.data(), ctx->aw_sync, h.size() * sizeof(unsigned), hipMemcpyDeviceToHost));
     for (int l = 0; l < ctx->c.n_layers; l++)
-        if (h[4 * l + 2]) return set_err(ctx, XH_E_HIP, "layer %d: attention -> Wo hand-off timed out", l);
+        if (h[(size_t)AW_SYNC_WORDS * l + 2]) return set_err(ctx, XH_E_HIP, "layer %d: attention -> Wo hand-off timed out", l);
     return 0;
 }
 
@@ -701,7 +701,7 @@ int xh_create(const xh_config* cfg, int device_ordinal, xh_ctx** out) {
     CREATE_TRY(dmalloc(ctx, &ctx->part_o, (size_t)ctx->nsplit * ctx->q_dim));
     CREATE_TRY(dmalloc(ctx, &ctx->part_ml, (size_t)ctx->nsplit * c.n_heads * 2));
     CREATE_TRY(dmalloc(ctx, &ctx->attn_cnt, (size_t)c.n_kv_heads));
-    CREATE_TRY(dmalloc(ctx, &ctx->aw_sync, (size_t)c.n_layers * 4));
+    CREATE_TRY(dmalloc(ctx, &ctx->aw_sync, (size_t)c.n_layers * AW_SYNC_WORDS));
     CREATE_TRY(dmalloc(ctx, &ctx->qaw_sync, qaw_words(c)));
     CREATE_TRY(dmalloc(ctx, &ctx->cand, (size_t)ARGMAX_CANDS));
     CREATE_TRY(dmalloc(ctx, &ctx->scan_flag, (size_t)1));
