@@ -159,6 +159,8 @@ def main():
     ap.add_argument("--kernel-iters", type=int, default=200)
     ap.add_argument("--engine", type=int, default=-1, choices=(-1, 0, 1),
                     help="-1 auto (persistent kernel when instantiated), 0 graph of kernels, 1 persistent")
+    ap.add_argument("--prefill-tokens", type=int, default=512,
+                    help="also time xh_prefill of this many prompt tokens (batched f32-MFMA path; 0 = skip)")
     ap.add_argument("--fuse-attn-wo", type=int, default=1, choices=(0, 1, 2),
                     help="graph engine: qkv + attention + Wo in one launch (2), attention + Wo (1), none (0)")
     args = ap.parse_args()
@@ -233,6 +235,26 @@ def main():
         b = model.kernel_bytes(which, kv_len_now)
         extra_kernels[name] = {"avg_us": round(us, 2), "GBps": round(b / (us * 1e-6) / 1e9, 1)}
 
+    # prompt processing, reported beside the decode metric: xh_prefill of a
+    # synthetic prompt at positions 0.. (overwrites the ring rows the decode used; timed last)
+    prefill = None
+    if args.prefill_tokens and not w["kv_prefill"] and args.prefill_tokens <= c.max_seq_len:
+        ptoks = prompt_tokens(c.vocab_size, n=args.prefill_tokens, seed=11)
+        model.prefill(ptoks[:64], 0, st)  # warm: buffers, code objects
+        sync_all(None, torch_mod)
+        t0 = time.perf_counter()
+        model.prefill(ptoks, 0, st)
+        sync_all(None, torch_mod)
+        pf_s = time.perf_counter() - t0
+        q_dim, kv_dim = c.n_heads * c.head_dim, c.n_kv_heads * c.head_dim
+        layer_params = c.dim * (q_dim + 2 * kv_dim) + q_dim * c.dim + 3 * c.dim * c.hidden_dim
+        flops = 2.0 * args.prefill_tokens * c.n_layers * layer_params  # matrix products only
+        prefill = {"tokens": args.prefill_tokens, "ms": round(pf_s * 1e3, 2),
+                   "tok_s": round(args.prefill_tokens / pf_s, 1),
+                   "mode": "batched" if model.get_option(L.OPT_PREFILL) else "per-token",
+                   "note": "passes of 64 tokens; every matrix product on v_mfma_f32_32x32x2_f32 (f32 activations, "
+                           "as the reference); f32 MFMA peak 157 TF/s", "matmul_tflops": round(flops / pf_s / 1e12, 1)}
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not w["kv_prefill"]:
         n = min(args.cpu_tokens, len(warm_tokens)) if warm_tokens else 0
@@ -279,6 +301,7 @@ def main():
                          "note": "Model::active_bytes per token x tok/s, whole forward incl. launch gaps"},
             "kernels": extra_kernels,
             "cpu_baseline": cpu,
+            "prefill": prefill,
         }
         print(json.dumps(out), flush=True)
     model.close()

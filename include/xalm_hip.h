@@ -169,7 +169,10 @@ int xh_set_graphs(xh_ctx* ctx, int enable);
  * and Wo (+ residual) in ONE launch with in-launch hand-offs (qaw.h); 1 = qkv launch, then
  * attention + Wo in one launch (attn_wo.h); 0 = three launches.  Same math.  Level 2 falls
  * back to 1 where the shape is not instantiated; xh_get_option reports the level in effect. */
-enum xh_option { XH_OPT_FUSE_ATTN_WO = 1 };
+/* XH_OPT_PREFILL (default 1): xh_prefill processes the prompt in passes of up to 64 tokens,
+ * each weight matrix streamed once per pass into f32-input MFMA GEMMs (prefill.h); 0 = one
+ * forward per token (the reference's loop, src/main.cpp:94-100).  Same math per token. */
+enum xh_option { XH_OPT_FUSE_ATTN_WO = 1, XH_OPT_PREFILL = 2 };
 int xh_set_option(xh_ctx* ctx, int option, int value);
 int xh_get_option(const xh_ctx* ctx, int option, int* value);
 

@@ -145,6 +145,50 @@ def test_prefill_matches_oracle(name, context, engine):
         assert np.abs(a - b).max() <= 2e-3 * max(1.0, np.abs(b).max())
 
 
+@pytest.mark.parametrize("name", FIXTURES)
+@pytest.mark.parametrize("n", [1, 37, 64, 150])
+def test_batched_prefill_matches_oracle(name, n):
+    """xh_prefill's batched path (prefill.h: f32-MFMA GEMMs over passes of <= 64 tokens,
+    causal attention per token) vs the oracle's token-by-token HYDRATE loop: last logits,
+    every layer's K and V rows, and the greedy continuation after it."""
+    xf = XalmFile(fixture_path(name + ".xalm"))
+    gm = Model.from_xalm(xf, context=256)
+    assert gm.get_option(L.OPT_PREFILL) == 1
+    om = O.OracleModel.from_xalm(xf, context=256)
+    toks = [1] + [3 + (i * 37) % 280 for i in range(n - 1)]
+    st = InferenceState(gm.config)
+    gm.prefill(toks, 0, st)
+    for pos, tok in enumerate(toks):
+        om.forward(tok, pos, L.OUTPUT_LOGITS if pos == len(toks) - 1 else L.HYDRATE_KV_CACHE)
+    assert np.abs(st.logits() - om.logits()).max() <= tol(om.logits())
+    for layer in range(gm.config.n_layers):
+        for which in (0, 1):
+            a = gm.kv_read(layer, which, 0, n).view(np.float16).astype(np.float32)
+            b = om.kv(layer, which)[:n].view(np.float16).astype(np.float32)
+            assert np.abs(a - b).max() <= 2e-3 * max(1.0, np.abs(b).max()), (layer, which)
+    nxt = gm.decode_greedy(n, 3)
+    gm.get_logits(st)
+    for i, t in enumerate(nxt):
+        om.forward(t, n + i)
+    assert np.abs(st.logits() - om.logits()).max() <= tol(om.logits())
+
+
+def test_batched_prefill_equals_token_loop():
+    """Batched and per-token prefill of the same prompt agree (logits and K/V rings)."""
+    xf = XalmFile(fixture_path("small_llama_f16.xalm"))
+    toks = [1] + [3 + (i * 53) % 300 for i in range(99)]
+    out = []
+    for mode in (1, 0):
+        gm = Model.from_xalm(xf, context=512)
+        gm.set_option(L.OPT_PREFILL, mode)
+        st = InferenceState(gm.config)
+        gm.prefill(toks, 0, st)
+        out.append((st.logits().copy(), gm.kv_read(1, 0, 0, len(toks)).view(np.float16).astype(np.float32)))
+        gm.close()
+    assert np.abs(out[0][0] - out[1][0]).max() <= tol(out[1][0])
+    assert np.abs(out[0][1] - out[1][1]).max() <= 2e-3 * max(1.0, np.abs(out[1][1]).max())
+
+
 def test_engines_agree_on_long_decode():
     # 200 greedy tokens on the head_dim-128 fixture: the persistent engine's tokens equal the
     # graph engine's (same per-row math; only the rmsnorm reduction order differs), logits

@@ -20,6 +20,7 @@ DTYPE_BY_NAME = {"F32": F32, "F16": F16, "BF16": BF16, "F8_E4M3": F8_E4M3, "F8_E
 DTYPE_SIZE = {F32: 4, F16: 2, BF16: 2, F8_E4M3: 1, F8_E5M2: 1, U8: 1, Q8: 1}
 # enum xh_option
 OPT_FUSE_ATTN_WO = 1
+OPT_PREFILL = 2
 
 # enum xh_tensor_kind
 EMBED, ATTN_NORM, FFN_NORM, WQ, WK, WV, WO, W1, W2, W3, FINAL_NORM, WCLS = range(12)

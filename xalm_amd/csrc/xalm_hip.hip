@@ -29,6 +29,7 @@
 #include "attention.h"
 #include "gemv.h"
 #include "dt_launch.h"
+#include "prefill.h"
 #include "standalone.h"
 
 using namespace xalm;
@@ -102,6 +103,17 @@ struct xh_ctx {
     unsigned* qaw_sync = nullptr;  // [n_layers][QAW_LAYER_WORDS] counters, then epoch, err
     int qaw_nsplit = 1, qaw_t_max = 16;
     bool qaw_ok = true;            // cleared when a launch reports the shape unsupported
+    // batched prefill (prefill.h), buffers allocated on first use
+    bool prefill_batched = true;
+    bool pf_alloc = false;
+    int* pf_tok = nullptr;                       // [PF_TOK]
+    float *pf_x = nullptr, *pf_xn = nullptr;     // [PF_TOK][dim]
+    float *pf_q = nullptr, *pf_att = nullptr;    // [PF_TOK][q_dim]
+    float* pf_h = nullptr;                       // [PF_TOK][hidden]
+    float* pf_part = nullptr;                    // [PF_PART_ROWS][PF_TOK] split-K partials
+    StepParams* pf_sp = nullptr;                 // [PF_TOK] per-token attention scalars
+    float *pf_po = nullptr, *pf_pml = nullptr;   // [PF_TOK][nsplit][q_dim], [PF_TOK][nsplit][n_heads][2]
+    int* pf_cnt = nullptr;                       // [PF_TOK][n_kv_heads] split tickets
     int t_max_aw = 16;
     bool use_graphs = true;
     hipGraphExec_t g_logits = nullptr, g_hydrate = nullptr, g_decode = nullptr;
@@ -418,13 +430,16 @@ int check_aw(xh_ctx* ctx) {
 int enqueue_step(xh_ctx* ctx, hipStream_t s, bool with_logits, bool greedy = false) {
     const xh_config& c = ctx->c;
     const int mb = ctx->max_gemv_waves;
+    // the qaw counters expect one epoch per step that launches qaw in every layer
+    unsigned* epoch = ctx->fuse_level >= 2 && ctx->qaw_ok && aw_instantiated(c.head_dim, ctx->qpk) ? qaw_epoch(ctx)
+                                                                                                    : nullptr;
     if (greedy)
         hipLaunchKernelGGL(argmax_embed_kernel, dim3(1), dim3(ARGMAX_CANDS), 0, s, (const unsigned long long*)ctx->cand,
                            ctx->sp, ctx->dec_tokens, ctx->dec_cap, (const void*)ctx->embed, ctx->embed_dt, c.dim,
-                           ctx->x, qaw_epoch(ctx));
+                           ctx->x, epoch);
     else
         hipLaunchKernelGGL(embed_kernel, dim3((c.dim + 255) / 256), dim3(256), 0, s, (const void*)ctx->embed,
-                           ctx->embed_dt, c.dim, ctx->x, (const StepParams*)ctx->sp, qaw_epoch(ctx));
+                           ctx->embed_dt, c.dim, ctx->x, (const StepParams*)ctx->sp, epoch);
     for (int l = 0; l < c.n_layers; l++) {
         const LayerW& w = ctx->L[l];
         if (ctx->fuse_level >= 2 && ctx->qaw_ok && aw_instantiated(c.head_dim, ctx->qpk)) {
@@ -629,6 +644,187 @@ int host_step_params(xh_ctx* ctx, int token, int pos) {
     return 0;
 }
 
+// ---------------------------------------------------------------------------------------
+// batched prefill (prefill.h)
+// ---------------------------------------------------------------------------------------
+template <class T>
+int dmalloc(xh_ctx* ctx, T** p, size_t n);
+constexpr size_t PF_PART_ROWS = 65536;  // >= ks * rows of every GEMM (ks * ceil(rows/32) <= 2048)
+
+int pf_alloc(xh_ctx* ctx) {
+    if (ctx->pf_alloc) return 0;
+    const xh_config& c = ctx->c;
+    int rc;
+    if ((rc = dmalloc(ctx, &ctx->pf_tok, (size_t)PF_TOK)) || (rc = dmalloc(ctx, &ctx->pf_x, (size_t)PF_TOK * c.dim)) ||
+        (rc = dmalloc(ctx, &ctx->pf_xn, (size_t)PF_TOK * c.dim)) ||
+        (rc = dmalloc(ctx, &ctx->pf_q, (size_t)PF_TOK * ctx->q_dim)) ||
+        (rc = dmalloc(ctx, &ctx->pf_att, (size_t)PF_TOK * ctx->q_dim)) ||
+        (rc = dmalloc(ctx, &ctx->pf_h, (size_t)PF_TOK * c.hidden_dim)) ||
+        (rc = dmalloc(ctx, &ctx->pf_part, PF_PART_ROWS * PF_TOK)) || (rc = dmalloc(ctx, &ctx->pf_sp, (size_t)PF_TOK)) ||
+        (rc = dmalloc(ctx, &ctx->pf_po, (size_t)PF_TOK * ctx->nsplit * ctx->q_dim)) ||
+        (rc = dmalloc(ctx, &ctx->pf_pml, (size_t)PF_TOK * ctx->nsplit * c.n_heads * 2)) ||
+        (rc = dmalloc(ctx, &ctx->pf_cnt, (size_t)PF_TOK * c.n_kv_heads)))
+        return rc;
+    ctx->pf_alloc = true;
+    return 0;
+}
+
+// K slices for a GEMM of `rows` outputs: about 2048 waves, K divisible into whole chunk pairs
+int pf_ks(int rows, int K, int E) {
+    const int n_rt = (rows + 31) / 32;
+    int ks = 1;
+    while (ks < 64 && (size_t)2 * ks * n_rt <= 2048 && K % (2 * ks * 2 * E) == 0) ks *= 2;
+    return ks;
+}
+
+template <int DT>
+void pf_gemm_t(const PfGemmArgs& a, hipStream_t s) {
+    const int waves = (a.rows + 31) / 32 * a.ks;
+    hipLaunchKernelGGL(prefill_gemm_kernel<DT>, dim3((waves + PF_WAVES - 1) / PF_WAVES), dim3(PF_THREADS), 0, s, a);
+}
+// Y partials of W[rows][K] . X[n][K]; returns ks (0: dtype / shape not supported)
+int pf_gemm(xh_ctx* ctx, int dt, const void* w, int K, int rows, const float* x, int n) {
+    const int E = (dt == XH_F8_E4M3_EXACT || dt == XH_F8_E5M2_EXACT) ? 16 : elems_per_16b(dt);
+    if (K % (2 * E)) return 0;
+    PfGemmArgs a{};
+    a.w = w; a.K = K; a.rows = rows; a.x = x; a.n = n; a.part = ctx->pf_part;
+    a.row_bytes = (size_t)K * (16 / E);
+    a.ks = pf_ks(rows, K, E);
+    if ((size_t)a.ks * rows > PF_PART_ROWS) return 0;
+    hipStream_t s = ctx->stream;
+    switch (dt) {
+        case XH_F32: pf_gemm_t<XH_F32>(a, s); break;
+        case XH_F16: pf_gemm_t<XH_F16>(a, s); break;
+        case XH_BF16: pf_gemm_t<XH_BF16>(a, s); break;
+        case XH_F8_E4M3: pf_gemm_t<XH_F8_E4M3>(a, s); break;
+        case XH_F8_E5M2: pf_gemm_t<XH_F8_E5M2>(a, s); break;
+        case XH_Q8: pf_gemm_t<XH_Q8>(a, s); break;
+        case XH_F8_E4M3_EXACT: pf_gemm_t<XH_F8_E4M3_EXACT>(a, s); break;
+        case XH_F8_E5M2_EXACT: pf_gemm_t<XH_F8_E5M2_EXACT>(a, s); break;
+        default: return 0;
+    }
+    return a.ks;
+}
+void pf_epi(xh_ctx* ctx, PfEpiArgs e) {
+    e.part = ctx->pf_part;
+    const int threads = e.n * (e.rows / 2);
+    hipLaunchKernelGGL(prefill_epi_kernel, dim3((threads + 255) / 256), dim3(256), 0, ctx->stream, e);
+}
+template <int HD, int QPK>
+void pf_attn_t(xh_ctx* ctx, const AttnArgs& a, int n) {
+    const size_t smem = attn_smem_bytes(HD, QPK, ctx->t_max, a.nsplit);
+    auto k = prefill_attn_kernel<HD, QPK>;
+    if (smem > 64 * 1024) {
+        static bool done = false;
+        if (!done) {
+            hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            done = true;
+        }
+    }
+    hipLaunchKernelGGL(k, dim3(ctx->c.n_kv_heads, a.nsplit, n), dim3(ATTN_THREADS), smem, ctx->stream, a,
+                       (const StepParams*)ctx->pf_sp, ctx->q_dim, ctx->c.n_kv_heads);
+}
+bool pf_attn(xh_ctx* ctx, const AttnArgs& a, int n) {
+    const int hd = ctx->c.head_dim, qpk = ctx->qpk;
+    if (hd == 128 && qpk == 4) pf_attn_t<128, 4>(ctx, a, n);
+    else if (hd == 128 && qpk == 8) pf_attn_t<128, 8>(ctx, a, n);
+    else if (hd == 64 && qpk == 4) pf_attn_t<64, 4>(ctx, a, n);
+    else if (hd == 16 && qpk == 2) pf_attn_t<16, 2>(ctx, a, n);
+    else return false;
+    return true;
+}
+
+// Whether the batched path covers this prompt (else the per-token loop): no ring wrap inside
+// the prompt, an instantiated head shape, K multiples of the chunk pair (always, for K % 32).
+bool pf_supported(const xh_ctx* ctx, int n, int pos0) {
+    const xh_config& c = ctx->c;
+    if (!ctx->prefill_batched || pos0 + n > c.max_seq_len) return false;
+    const int hd = c.head_dim, qpk = ctx->qpk;
+    if (!((hd == 128 && (qpk == 4 || qpk == 8)) || (hd == 64 && qpk == 4) || (hd == 16 && qpk == 2))) return false;
+    return c.dim % 32 == 0 && c.hidden_dim % 32 == 0 && ctx->q_dim % 32 == 0;
+}
+
+// tokens[0..n) at positions pos0..: HYDRATE for every token, then the last token's logits
+int prefill_batched(xh_ctx* ctx, const int* tokens, int n, int pos0, int want_logits) {
+    const xh_config& c = ctx->c;
+    int rc = pf_alloc(ctx);
+    if (rc) return rc;
+    std::vector<StepParams> sps(PF_TOK);
+    for (int off = 0; off < n; off += PF_TOK) {
+        const int m = std::min(n - off, PF_TOK);
+        const int p0 = pos0 + off;
+        HIP_TRY(ctx, hipMemcpyAsync(ctx->pf_tok, tokens + off, (size_t)m * sizeof(int), hipMemcpyHostToDevice, ctx->stream));
+        for (int t = 0; t < m; t++) {
+            StepParams& h = sps[t];
+            h = StepParams{};
+            h.token = tokens[off + t];
+            h.pos = p0 + t;
+            h.kv_sink = 0;
+            h.kv_pos = p0 + t;
+            h.kv_len = p0 + t + 1;
+            h.max_seq_len = c.max_seq_len;
+        }
+        HIP_TRY(ctx, hipMemcpyAsync(ctx->pf_sp, sps.data(), (size_t)m * sizeof(StepParams), hipMemcpyHostToDevice,
+                                    ctx->stream));
+        hipLaunchKernelGGL(prefill_embed_kernel, dim3(m), dim3(256), 0, ctx->stream, (const int*)ctx->pf_tok,
+                           (const void*)ctx->embed, ctx->embed_dt, c.dim, ctx->pf_x);
+        for (int l = 0; l < c.n_layers; l++) {
+            const LayerW& w = ctx->L[l];
+            // attention block (src/infer.cpp:380-452)
+            hipLaunchKernelGGL(prefill_rmsnorm_kernel, dim3(m), dim3(256), 0, ctx->stream, (const float*)ctx->pf_x, c.dim,
+                               (const void*)w.attn_norm, w.an_dt, c.norm_eps, ctx->pf_xn);
+            const int qkv_rows = ctx->q_dim + 2 * ctx->kv_dim;
+            int ks = pf_gemm(ctx, kdt(w.qkv_dt, w.qkv_x), w.wqkv, c.dim, qkv_rows, ctx->pf_xn, m);
+            if (!ks) return set_err(ctx, XH_E_INVALID, "prefill: qkv shape not supported");
+            PfEpiArgs e{};
+            e.ks = ks; e.n = m; e.rows = qkv_rows; e.epi = EPI_QKV; e.q = ctx->pf_q;
+            e.kcache = ctx->kcache(l); e.vcache = ctx->vcache(l); e.q_dim = ctx->q_dim; e.kv_dim = ctx->kv_dim;
+            e.head_dim = c.head_dim; e.rope_freq = ctx->rope_freq; e.qkv_clip = c.qkv_clip; e.pos0 = p0; e.act = c.act;
+            pf_epi(ctx, e);
+            AttnArgs aa = attn_args(ctx, l);
+            aa.q = ctx->pf_q; aa.out = ctx->pf_att; aa.part_o = ctx->pf_po; aa.part_ml = ctx->pf_pml;
+            aa.counters = ctx->pf_cnt; aa.nsplit = ctx->nsplit;
+            if (!pf_attn(ctx, aa, m)) return set_err(ctx, XH_E_INVALID, "prefill: head shape not instantiated");
+            ks = pf_gemm(ctx, kdt(w.wo_dt, w.wo_x), w.wo, ctx->q_dim, c.dim, ctx->pf_att, m);
+            if (!ks) return set_err(ctx, XH_E_INVALID, "prefill: wo shape not supported");
+            e = PfEpiArgs{};
+            e.ks = ks; e.n = m; e.rows = c.dim; e.epi = EPI_RESID; e.out = ctx->pf_x;
+            pf_epi(ctx, e);
+            // feed-forward block (src/infer.cpp:455-494)
+            hipLaunchKernelGGL(prefill_rmsnorm_kernel, dim3(m), dim3(256), 0, ctx->stream, (const float*)ctx->pf_x, c.dim,
+                               (const void*)w.ffn_norm, w.fn_dt, c.norm_eps, ctx->pf_xn);
+            ks = pf_gemm(ctx, kdt(w.w13_dt, w.w13_x), w.w13, c.dim, 2 * c.hidden_dim, ctx->pf_xn, m);
+            if (!ks) return set_err(ctx, XH_E_INVALID, "prefill: w1/w3 shape not supported");
+            e = PfEpiArgs{};
+            e.ks = ks; e.n = m; e.rows = 2 * c.hidden_dim; e.epi = EPI_GLU; e.out = ctx->pf_h; e.act = c.act;
+            pf_epi(ctx, e);
+            ks = pf_gemm(ctx, kdt(w.w2_dt, w.w2_x), w.w2, c.hidden_dim, c.dim, ctx->pf_h, m);
+            if (!ks) return set_err(ctx, XH_E_INVALID, "prefill: w2 shape not supported");
+            e = PfEpiArgs{};
+            e.ks = ks; e.n = m; e.rows = c.dim; e.epi = EPI_RESID; e.out = ctx->pf_x;
+            pf_epi(ctx, e);
+        }
+        HIP_TRY(ctx, hipGetLastError());
+        if (off + m == n) {
+            // the last token's residual stream is the decode path's x
+            HIP_TRY(ctx, hipMemcpyAsync(ctx->x, ctx->pf_x + (size_t)(m - 1) * c.dim, (size_t)c.dim * 4,
+                                        hipMemcpyDeviceToDevice, ctx->stream));
+        }
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));  // sps / token staging reused by the next pass
+    }
+    // step parameters of the last prompt token (as the per-token loop leaves them)
+    rc = host_step_params(ctx, tokens[n - 1], pos0 + n - 1);
+    if (rc) return rc;
+    if (want_logits) {
+        if (!launch_gemv<PRO_RMSNORM, EPI_LOGITS>(kdt(ctx->wcls_dt, ctx->wcls_x), cls_args(ctx), ctx->stream,
+                                                   ctx->max_gemv_waves))
+            return set_err(ctx, XH_E_INVALID, "unsupported wcls dtype");
+        ctx->cand_valid = true;
+    }
+    HIP_TRY(ctx, hipGetLastError());
+    return 0;
+}
+
 template <typename T>
 int dmalloc(xh_ctx* ctx, T** p, size_t n) {
     HIP_TRY(ctx, hipMalloc((void**)p, n ? n * sizeof(T) : 16));
@@ -784,7 +980,9 @@ void xh_destroy(xh_ctx* ctx) {
     if (ctx->wcls && ctx->wcls != ctx->embed) hipFree(ctx->wcls);
     hipFree(ctx->embed); hipFree(ctx->final_norm);
     hipFree(ctx->kv); hipFree(ctx->x); hipFree(ctx->q); hipFree(ctx->attn_out); hipFree(ctx->hb);
-    hipFree(ctx->logits); hipFree(ctx->part_o); hipFree(ctx->part_ml); hipFree(ctx->attn_cnt); hipFree(ctx->aw_sync); hipFree(ctx->qaw_sync); hipFree(ctx->cand); hipFree(ctx->scan_flag); hipFree(ctx->rope_freq);
+    hipFree(ctx->logits); hipFree(ctx->part_o); hipFree(ctx->part_ml); hipFree(ctx->attn_cnt); hipFree(ctx->aw_sync); hipFree(ctx->qaw_sync); hipFree(ctx->cand); hipFree(ctx->scan_flag);
+    hipFree(ctx->pf_tok); hipFree(ctx->pf_x); hipFree(ctx->pf_xn); hipFree(ctx->pf_q); hipFree(ctx->pf_att); hipFree(ctx->pf_h);
+    hipFree(ctx->pf_part); hipFree(ctx->pf_sp); hipFree(ctx->pf_po); hipFree(ctx->pf_pml); hipFree(ctx->pf_cnt); hipFree(ctx->rope_freq);
     hipFree(ctx->pk_layers); hipFree(ctx->pk_counters); hipFree(ctx->pk_tickets); hipFree(ctx->pk_err);
     hipFree(ctx->pk_cand); hipFree(ctx->pk_prompt); hipFree(ctx->pk_trace);
     if (ctx->pk_host) hipHostFree(ctx->pk_host);
@@ -1160,6 +1358,8 @@ int xh_prefill(xh_ctx* ctx, const int* tokens, int n, int pos0, int want_logits,
             const int m = std::min(n - off, ctx->pk_prompt_cap);
             rc = run_persistent(ctx, tokens + off, m, 0, pos0 + off, off + m == n ? want_logits : 0, -1, -1, nullptr);
         }
+    } else if (pf_supported(ctx, n, pos0)) {
+        rc = prefill_batched(ctx, tokens, n, pos0, want_logits);
     } else {
         for (int i = 0; i < n && !rc; i++) {
             rc = host_step_params(ctx, tokens[i], pos0 + i);
@@ -1220,6 +1420,7 @@ int xh_get_option(const xh_ctx* ctx, int option, int* value) {
             *value = ctx->fuse_level >= 2 && ctx->qaw_ok && aw_instantiated(ctx->c.head_dim, ctx->qpk) ? 2
                      : ctx->fuse_attn_wo ? 1 : 0;
             return 0;
+        case XH_OPT_PREFILL: *value = ctx->prefill_batched ? 1 : 0; return 0;
         default: return XH_E_INVALID;
     }
 }
@@ -1237,6 +1438,9 @@ int xh_set_option(xh_ctx* ctx, int option, int value) {
             ctx->fuse_attn_wo = value != 0;
             ctx->fuse_level = value;
             drop_graphs(ctx);
+            return 0;
+        case XH_OPT_PREFILL:
+            ctx->prefill_batched = value != 0;
             return 0;
         default: return set_err(ctx, XH_E_INVALID, "unknown option %d", option);
     }
