@@ -269,7 +269,9 @@ def main():
                     "kernel": "persistent_decode_kernel (all phases of all timed tokens, one launch)",
                     "bytes_per_launch": step_bytes, "avg_launch_us": round(launch_us, 1)}
     else:
-        traffic, src = pmc_traffic("void xalm::gemv_kernel<%d, 1, 3," % w["wdt"])
+        # the W1/W3 launch's exact instantiation (PF shape, see xalm_hip.hip launch_gemv_t)
+        traffic, src = pmc_traffic("void xalm::gemv_kernel<%d, 1, 3, xalm::GemvShape<512, 2, 4, true, 4, true, 2> >"
+                                   % w["wdt"])
         roofline = {"bound": "hbm", "achieved": round(k_gbps, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                     "frac": round(k_gbps / HBM_PEAK_GBPS, 4), "traffic": traffic,
                     "traffic_source": src,

@@ -1,0 +1,35 @@
+#!/bin/bash
+# Round evidence on the GPU box: PMC traffic passes, rocprofv3 kernel stats, and bench lines for
+# every BASELINE workload.  Output: gpurun_out/$ROUND/ (copy into profiles/ as ${ROUND}_*).
+# Each GPU step has its own limit; a crash / abort / timeout ends the run.
+set -u
+cd "$(dirname "$0")/.."
+ROUND=${ROUND:-r01}
+OUT=gpurun_out/$ROUND
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+step() {
+    local name=$1 limit=$2
+    shift 2
+    echo "== $name $(date +%T)"
+    timeout -k 10 "$limit" "$@" > "$OUT/$name.log" 2>&1
+    local rc=$?
+    echo "== $name rc=$rc"
+    if [ $rc -ne 0 ]; then tail -5 "$OUT/$name.log"; exit $rc; fi
+}
+# HBM traffic (MI355X_MICROARCH.md HBM section): FETCH_SIZE and WRITE_SIZE in separate passes
+for c in FETCH_SIZE WRITE_SIZE; do
+    step pmc_$c 300 rocprofv3 --pmc $c --kernel-trace -d "$OUT/pmc/$c" -o run --output-format csv -- \
+        python3 bench.py --steps 16 --warmup 2 --no-cpu-baseline --kernel-iters 10 --prefill-tokens 0
+done
+python3 tools/pmc_summary.py "$OUT/pmc" > "$OUT/pmc.json"
+cp "$OUT/pmc.json" "profiles/${ROUND}_pmc.json"   # read by bench.py's roofline.traffic
+step kernel_trace 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
+    python3 bench.py --steps 64 --warmup 4 --no-cpu-baseline --kernel-iters 50 --prefill-tokens 0
+cp "$OUT/prof/run_kernel_stats.csv" "$OUT/kernel_stats.csv"
+step bench 600 python3 bench.py
+step bench_f8 600 python3 bench.py --workload mistral-7b-f8
+step bench_32k 600 python3 bench.py --workload mistral-7b-f16-32k --steps 64
+step bench_llama 600 python3 bench.py --workload llama3-8b-f16
+for b in bench bench_f8 bench_32k bench_llama; do tail -1 "$OUT/$b.log" > "$OUT/$b.json"; done
+echo "== done"
