@@ -64,12 +64,9 @@ static void run_completion(const std::string& path, Device dev, const std::strin
     const size_t n_prompt = encoding.size();
     const auto t0 = clk::now();
     size_t read_bytes = 0;
-    for (size_t pos = 0; pos < encoding.size(); pos++) {
-        const InferenceMode mode =
-            pos + 1 == encoding.size() ? InferenceMode::OUTPUT_LOGITS : InferenceMode::HYDRATE_KV_CACHE;
-        model.forward(state, encoding[pos], (int)pos, mode);
-        read_bytes += model.active_bytes(pos);
-    }
+    // the hydrate loop (src/main.cpp:94-100) as one xh_prefill call
+    model.prefill(state, encoding, 0);
+    for (size_t pos = 0; pos < encoding.size(); pos++) read_bytes += model.active_bytes(pos);
     const auto t1 = clk::now();
     if (device_loop && num_steps > 0) {
         const std::vector<int> gen = model.decode_greedy((int)encoding.size(), num_steps, tokenizer.eos_id,

@@ -71,6 +71,11 @@ void Model::forward(InferenceState& s, const int token, const int pos, const Inf
     check(xh_forward(_ctx, token, pos, (int)mode, out), _ctx, "xh_forward");
 }
 
+void Model::prefill(InferenceState& s, const std::vector<int>& tokens, const int pos0) const {
+    if (tokens.empty()) return;
+    check(xh_prefill(_ctx, tokens.data(), (int)tokens.size(), pos0, 1, s.logits()), _ctx, "xh_prefill");
+}
+
 std::vector<int> Model::decode_greedy(const int pos, const int n_steps, const int stop_a, const int stop_b) const {
     std::vector<int> toks((size_t)std::max(n_steps, 1));
     int done = 0;

@@ -91,6 +91,9 @@ public:
     Config config;
 
     void forward(InferenceState& s, int token, int pos, InferenceMode mode = InferenceMode::OUTPUT_LOGITS) const;
+    // the prompt loop (src/main.cpp:94-100) in one call: HYDRATE tokens[0..n-1), the last with
+    // logits into s (xh_prefill: batched passes of up to 64 tokens)
+    void prefill(InferenceState& s, const std::vector<int>& tokens, int pos0) const;
     // greedy decode on the device (no host round trip per token); returns the tokens
     std::vector<int> decode_greedy(int pos, int n_steps, int stop_a = -1, int stop_b = -1) const;
     void fetch_logits(InferenceState& s) const;
