@@ -11,7 +11,9 @@
 // streams 16 bytes of row r0 + (l & 31) at k = kb + E (l >> 5) and decodes them to E floats:
 // they are the B operand of E MFMAs whose A operand is X[t][same k] (MFMA 32x32x2 f32 operand
 // map: A[i = l & 31][k = l >> 5], B[k = l >> 5][j = l & 31]), so weights go HBM -> VGPR ->
-// MFMA with no LDS staging; X (a few MB) is read from L2.  K slices write f32 partials
+// MFMA with no LDS staging; X (a few MB) is read from L2 (a transposed X^T layout, whose
+// A-operand loads read whole 128-B lines, measured no faster: +1 % f16, -7 % fp8).  K slices
+// write f32 partials
 // [slice][t][r]; a second kernel sums them in slice order and applies the decode path's
 // epilogue (clip + rope + fp16 K/V write, silu * up, residual add).
 #pragma once
@@ -38,7 +40,8 @@ struct PfGemmArgs {
     float* part;       // [ks][n][rows]
 };
 
-template <int DT>
+// PIPE: K slice a multiple of 4 chunk pairs (weights requested 4 pairs ahead)
+template <int DT, bool PIPE>
 __global__ __launch_bounds__(PF_THREADS) void prefill_gemm_kernel(const PfGemmArgs a) {
     constexpr int E = WDec<DT>::E;
     constexpr int ESZ = 16 / E;  // bytes per element
@@ -57,28 +60,75 @@ __global__ __launch_bounds__(PF_THREADS) void prefill_gemm_kernel(const PfGemmAr
     const float* x0 = a.x + (size_t)min(j, a.n - 1) * a.K;
     const float* x1 = a.x + (size_t)min(32 + j, a.n - 1) * a.K;
     f32x16 acc0 = {}, acc1 = {};
-    for (int kb = k0; kb < k1; kb += 2 * E) {
+    // software pipeline over chunk pairs: (weights, X) of later pairs in flight while this
+    // one's 2E MFMAs run (weights come from HBM, X from L2)
+    struct Stage {
+        u32x4 w;
+        float4 x0[E / 4], x1[E / 4];
+    };
+    auto load = [&](Stage& st, const int kb) {
         const int k = kb + E * h;
-        const u32x4 wv = *(const u32x4*)(wrow + (size_t)k * ESZ);
+        st.w = *(const u32x4*)(wrow + (size_t)k * ESZ);
+#pragma unroll
+        for (int q = 0; q < E / 4; q++) st.x0[q] = *(const float4*)(x0 + k + 4 * q);
+        if (n_tt > 1) {
+#pragma unroll
+            for (int q = 0; q < E / 4; q++) st.x1[q] = *(const float4*)(x1 + k + 4 * q);
+        }
+    };
+    auto mfma = [&](const Stage& st) {
         float wf[E];
-        WDec<DT>::dec(wv, wf);
-        float xa[E];
+        WDec<DT>::dec(st.w, wf);
 #pragma unroll
         for (int q = 0; q < E / 4; q++) {
-            const float4 v = *(const float4*)(x0 + k + 4 * q);
-            xa[4 * q] = v.x; xa[4 * q + 1] = v.y; xa[4 * q + 2] = v.z; xa[4 * q + 3] = v.w;
+            acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(st.x0[q].x, wf[4 * q + 0], acc0, 0, 0, 0);
+            acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(st.x0[q].y, wf[4 * q + 1], acc0, 0, 0, 0);
+            acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(st.x0[q].z, wf[4 * q + 2], acc0, 0, 0, 0);
+            acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(st.x0[q].w, wf[4 * q + 3], acc0, 0, 0, 0);
         }
-#pragma unroll
-        for (int e = 0; e < E; e++) acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(xa[e], wf[e], acc0, 0, 0, 0);
         if (n_tt > 1) {
 #pragma unroll
             for (int q = 0; q < E / 4; q++) {
-                const float4 v = *(const float4*)(x1 + k + 4 * q);
-                xa[4 * q] = v.x; xa[4 * q + 1] = v.y; xa[4 * q + 2] = v.z; xa[4 * q + 3] = v.w;
+                acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(st.x1[q].x, wf[4 * q + 0], acc1, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(st.x1[q].y, wf[4 * q + 1], acc1, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(st.x1[q].z, wf[4 * q + 2], acc1, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(st.x1[q].w, wf[4 * q + 3], acc1, 0, 0, 0);
             }
-#pragma unroll
-            for (int e = 0; e < E; e++) acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(xa[e], wf[e], acc1, 0, 0, 0);
         }
+    };
+    if (PIPE) {
+        // 4-deep ring of (weights, X) chunk pairs: a wave's loads complete in issue order
+        // (vmcnt), so X travels with its weights and waiting for chunk c leaves c+1..c+3 in
+        // flight.  (k1 - k0) % (8E) == 0 (host-checked); indices clamped so every load is
+        // unconditional (the last chunk is re-read past the end, unused)
+        const int P = (k1 - k0) / (2 * E);
+        auto ld = [&](Stage& st, const int c) { load(st, k0 + 2 * E * min(c, P - 1)); };
+        Stage s0, s1, s2, s3;
+        ld(s0, 0);
+        ld(s1, 1);
+        ld(s2, 2);
+        ld(s3, 3);
+        for (int c = 0; c < P; c += 4) {
+            mfma(s0);
+            ld(s0, c + 4);
+            mfma(s1);
+            ld(s1, c + 5);
+            mfma(s2);
+            ld(s2, c + 6);
+            mfma(s3);
+            ld(s3, c + 7);
+        }
+    } else {
+        Stage sa, sb;
+        int kb = k0;
+        load(sa, kb);
+        for (; kb + 4 * E <= k1; kb += 4 * E) {
+            load(sb, kb + 2 * E);
+            mfma(sa);
+            if (kb + 4 * E < k1) load(sa, kb + 4 * E);
+            mfma(sb);
+        }
+        if (kb < k1) mfma(sa);  // odd count of chunk pairs: the last one, loaded above
     }
     if (r >= a.rows) return;
     // D map: column j = lane & 31 (row r), row i = (reg & 3) + 8 (reg >> 2) + 4 h (token)

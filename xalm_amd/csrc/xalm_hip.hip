@@ -649,7 +649,8 @@ int host_step_params(xh_ctx* ctx, int token, int pos) {
 // ---------------------------------------------------------------------------------------
 template <class T>
 int dmalloc(xh_ctx* ctx, T** p, size_t n);
-constexpr size_t PF_PART_ROWS = 65536;  // >= ks * rows of every GEMM (ks * ceil(rows/32) <= 2048)
+constexpr int PF_WAVE_TARGET = 2048;  // 2 waves per SIMD (4096 measured slower: more split-K partials)
+constexpr size_t PF_PART_ROWS = 32 * PF_WAVE_TARGET;  // >= ks * rows of every GEMM (ks * ceil(rows/32) <= target)
 
 int pf_alloc(xh_ctx* ctx) {
     if (ctx->pf_alloc) return 0;
@@ -669,18 +670,26 @@ int pf_alloc(xh_ctx* ctx) {
     return 0;
 }
 
-// K slices for a GEMM of `rows` outputs: about 2048 waves, K divisible into whole chunk pairs
+// K slices for a GEMM of `rows` outputs: about PF_WAVE_TARGET waves, K divisible into whole
+// chunk pairs
 int pf_ks(int rows, int K, int E) {
     const int n_rt = (rows + 31) / 32;
     int ks = 1;
-    while (ks < 64 && (size_t)2 * ks * n_rt <= 2048 && K % (2 * ks * 2 * E) == 0) ks *= 2;
+    // slices stay whole multiples of 4 chunk pairs (the pipelined kernel) where K allows
+    const int unit = K % (8 * E) == 0 ? 8 * E : 2 * E;
+    while (ks < 64 && (size_t)2 * ks * n_rt <= PF_WAVE_TARGET && K % (2 * ks * unit) == 0) ks *= 2;
     return ks;
 }
 
 template <int DT>
 void pf_gemm_t(const PfGemmArgs& a, hipStream_t s) {
     const int waves = (a.rows + 31) / 32 * a.ks;
-    hipLaunchKernelGGL(prefill_gemm_kernel<DT>, dim3((waves + PF_WAVES - 1) / PF_WAVES), dim3(PF_THREADS), 0, s, a);
+    constexpr int E = WDec<DT>::E;
+    const dim3 grid((waves + PF_WAVES - 1) / PF_WAVES);
+    if ((a.K / a.ks) % (8 * E) == 0)
+        hipLaunchKernelGGL((prefill_gemm_kernel<DT, true>), grid, dim3(PF_THREADS), 0, s, a);
+    else
+        hipLaunchKernelGGL((prefill_gemm_kernel<DT, false>), grid, dim3(PF_THREADS), 0, s, a);
 }
 // Y partials of W[rows][K] . X[n][K]; returns ks (0: dtype / shape not supported)
 int pf_gemm(xh_ctx* ctx, int dt, const void* w, int K, int rows, const float* x, int n) {
@@ -783,7 +792,9 @@ int prefill_batched(xh_ctx* ctx, const int* tokens, int n, int pos0, int want_lo
             pf_epi(ctx, e);
             AttnArgs aa = attn_args(ctx, l);
             aa.q = ctx->pf_q; aa.out = ctx->pf_att; aa.part_o = ctx->pf_po; aa.part_ml = ctx->pf_pml;
-            aa.counters = ctx->pf_cnt; aa.nsplit = ctx->nsplit;
+            // splits for this pass's longest row (attn_block: >= ATTN_MIN_T slots per split)
+            aa.counters = ctx->pf_cnt;
+            aa.nsplit = std::min(ctx->nsplit, std::max(1, (p0 + m + ATTN_MIN_T - 1) / ATTN_MIN_T));
             if (!pf_attn(ctx, aa, m)) return set_err(ctx, XH_E_INVALID, "prefill: head shape not instantiated");
             ks = pf_gemm(ctx, kdt(w.wo_dt, w.wo_x), w.wo, ctx->q_dim, c.dim, ctx->pf_att, m);
             if (!ks) return set_err(ctx, XH_E_INVALID, "prefill: wo shape not supported");
