@@ -102,6 +102,14 @@ const char* xh_last_error(const xh_ctx* ctx); /* ctx may be NULL: last create er
  * the kernels fuse (q/k/v, gate/up) must share one dtype. */
 int xh_upload(xh_ctx* ctx, int tensor_kind, int layer, int dtype, const void* host, size_t bytes);
 
+/* The same upload read straight from a file: `bytes` at absolute `offset` of `path` (a
+ * .xalm tensor, convert.py:248-321; the reference reads it into a host Tensor first,
+ * src/xalm.h:90-192, src/model.cpp:48-118).  The range is memory-mapped, pinned for the
+ * copy and moved by one DMA; no host copy of the tensor is made.  Same validation as
+ * xh_upload, plus the range must lie inside the file.  Synchronous. */
+int xh_upload_file(xh_ctx* ctx, int tensor_kind, int layer, int dtype, const char* path, uint64_t offset,
+                   size_t bytes);
+
 /* Benchmark weights without a checkpoint: fill the tensor slot on the device with the
  * deterministic values of include/xalm_synth.h (element i of the logical [rows][cols]
  * tensor = xs_value(seed, i, mean, std) rounded to `dtype`).  The CPU baseline builds the

@@ -276,6 +276,77 @@ def test_upload_validation():
         gm.forward(st, 1, 0)  # weights missing
 
 
+@pytest.mark.parametrize("name", FIXTURES)
+def test_upload_file_equals_host_upload(name):
+    # xh_upload_file (pread into pinned staging + DMA) and xh_upload (host buffer) must leave
+    # the same bytes on the device: the logits agree bit for bit
+    xf = XalmFile(fixture_path(name + ".xalm"))
+    outs = []
+    for direct in (True, False):
+        gm = Model.from_xalm(xf, direct=direct)
+        st = InferenceState(gm.config)
+        got = []
+        for pos, tok in enumerate([1, 5, 9, 3]):
+            gm.forward(st, tok, pos)
+            got.append(st.logits().copy())
+        outs.append(np.stack(got))
+        gm.close()
+    assert np.array_equal(outs[0], outs[1])
+
+
+def test_upload_file_multi_chunk_strided(tmp_path):
+    # Mistral-7B gate/up shapes (f16 [14336, 4096] = 112 MiB each, at a nonzero file offset)
+    # into the interleaved W1/W3 slot: file upload vs host upload, bit-equal logits
+    cfg = L.XhConfig()
+    cfg.dim, cfg.hidden_dim, cfg.head_dim, cfg.n_layers = 4096, 14336, 128, 1
+    cfg.n_heads, cfg.n_kv_heads, cfg.vocab_size, cfg.max_seq_len = 32, 8, 512, 64
+    cfg.rope_theta, cfg.rotary_dim, cfg.norm_eps, cfg.act = 1e6, 128, 1e-5, L.ACT_SILU
+    cfg.qkv_clip, cfg.tie_word_embeddings = float(np.finfo(np.float32).max), 0
+    rng = np.random.default_rng(3)
+    w = {k: (rng.standard_normal((14336, 4096), dtype=np.float32) * 0.02).astype(np.float16).view(np.uint16)
+         for k in (L.W1, L.W3)}
+    path = tmp_path / "w13.bin"
+    with open(path, "wb") as f:
+        f.write(b"\0" * 96)  # a nonzero, 32-B aligned start, as in a .xalm file
+        for k in (L.W1, L.W3):
+            f.write(w[k].tobytes())
+    outs = []
+    for direct in (True, False):
+        gm = Model(cfg)
+        for i, kind in enumerate([L.EMBED, L.WQ, L.WK, L.WV, L.WO, L.W2, L.WCLS]):
+            gm.upload_synthetic(kind, 0, L.F16, 100 + i, 0.0, 1.0 if kind == L.EMBED else 0.02)
+        for kind in (L.ATTN_NORM, L.FFN_NORM, L.FINAL_NORM):
+            gm.upload_synthetic(kind, 0, L.BF16, 200 + kind, 1.0, 0.01)
+        for j, kind in enumerate((L.W1, L.W3)):
+            if direct:
+                gm.upload_file(kind, 0, L.F16, str(path), 96 + j * w[kind].nbytes, w[kind].nbytes)
+            else:
+                gm.upload(kind, 0, L.F16, w[kind])
+        st = InferenceState(cfg)
+        gm.forward(st, 7, 0)
+        outs.append(st.logits().copy())
+        gm.close()
+    assert np.isfinite(outs[0]).all()
+    assert np.array_equal(outs[0], outs[1])
+
+
+def test_upload_file_validation(tmp_path):
+    xf = XalmFile(fixture_path("tiny_mistral_f16.xalm"))
+    gm = Model(xf.config())
+    ti = xf.tensors["l.0.attn.q.weight"]
+    with pytest.raises(L.XhError):
+        gm.upload_file(L.WQ, 0, L.F16, str(tmp_path / "missing.xalm"), ti.offset, ti.size)
+    with pytest.raises(L.XhError):  # range past the end of the file
+        gm.upload_file(L.WQ, 0, L.F16, xf.path, ti.offset + 10 ** 9, ti.size)
+    with pytest.raises(L.XhError):  # wrong size
+        gm.upload_file(L.WQ, 0, L.F16, xf.path, ti.offset, ti.size - 2)
+    short = tmp_path / "short.bin"
+    short.write_bytes(b"\0" * 100)
+    with pytest.raises(L.XhError):
+        gm.upload_file(L.WQ, 0, L.F16, str(short), 0, ti.size)
+    gm.upload_file(L.WQ, 0, L.F16, xf.path, ti.offset, ti.size)  # the good call still works
+
+
 @pytest.mark.parametrize("engine", ENGINES)
 def test_multi_split_attention_in_model(engine):
     # -T 1024 on the head_dim-128 fixture: kv_len 300 runs attention in several splits whose

@@ -53,6 +53,7 @@ _SIGNATURES = {
     "xh_destroy": (None, [_P]),
     "xh_last_error": (ctypes.c_char_p, [_P]),
     "xh_upload": (_I, [_P, _I, _I, _I, _P, _SZ]),
+    "xh_upload_file": (_I, [_P, _I, _I, _I, ctypes.c_char_p, ctypes.c_uint64, _SZ]),
     "xh_upload_synthetic": (_I, [_P, _I, _I, _I, ctypes.c_uint64, ctypes.c_float, ctypes.c_float]),
     "xh_kv_fill_synthetic": (_I, [_P, _I, _I, _I, _I, ctypes.c_uint64, ctypes.c_float]),
     "xh_forward": (_I, [_P, _I, _I, _I, _P]),

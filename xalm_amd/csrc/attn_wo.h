@@ -174,7 +174,6 @@ __global__ __launch_bounds__(AW_THREADS) void attn_wo_kernel(const AttnArgs aa, 
         if (trace && threadIdx.x == 0) trace[8 * b + 1] = __builtin_amdgcn_s_memrealtime();
         return;
     }
-    float* red = (float*)smem;
     float4* xs4 = (float4*)(smem + LDS_HEAD_BYTES);
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int nb = gridDim.x - n_att;

@@ -5,18 +5,28 @@
 // ownership of Model::from_xalm (src/model.cpp:48-118).
 //
 // Per token the stream runs (all launches captured once into a hipGraph and replayed; the
-// token/position scalars live in device memory, StepParams):
-//   embed_kernel                                    x = embed[token]
+// token/position scalars live in device memory, StepParams). Default engine, fuse_level 1:
+//   embed_kernel (argmax_embed_kernel in the greedy graph)          x = embed[token]
 //   per layer:
 //     gemv<PRO_RMSNORM, EPI_QKV>    [Wq;Wk;Wv] (one fused matrix) + rmsnorm + clip + rope +
 //                                   fp16 K/V ring write + sink re-rotation
-//     attn_split_kernel             GQA attention over the ring (split-KV, in-kernel merge)
-//     gemv<PRO_PLAIN, EPI_RESID>    Wo, x += .
+//     attn_wo_kernel (attn_wo.h)    split-KV GQA attention; the last split of a KV head merges
+//                                   the partials, then Wo rows (x += .) in the same launch
 //     gemv<PRO_RMSNORM, EPI_GLU>    [W1;W3] rows interleaved + rmsnorm + silu(g)*u
 //     gemv<PRO_PLAIN, EPI_RESID>    W2, x += .
-//   gemv<PRO_RMSNORM, EPI_STORE>    final rmsnorm + lm_head -> logits   (OUTPUT_LOGITS only)
+//   gemv<PRO_RMSNORM, EPI_STORE>    final rmsnorm + lm_head -> logits   (OUTPUT_LOGITS)
+//   gemv<PRO_RMSNORM, EPI_LOGITS>   ... + per-workgroup argmax candidates (greedy graph)
+// fuse_level 0 launches attention and Wo separately; 2 runs qkv + attention + Wo in one launch
+// (qaw.h); engine 1 is the persistent whole-token kernel (persistent.h). Prompts go through
+// prefill.h (passes of 64 tokens on f32 MFMA) unless XH_OPT_PREFILL is 0.
 #include <hip/hip_runtime.h>
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
 
+#include <algorithm>
+#include <cerrno>
 #include <cfloat>
 #include <cmath>
 #include <cstdarg>
@@ -1149,6 +1159,28 @@ __global__ void synth_fill_kernel(char* base, size_t pitch, size_t rows, size_t 
     }
 }
 
+// the byte count of a tensor upload against the config (load_tensor's checks,
+// src/model.cpp:62-76), before the device layout is touched
+int check_bytes(xh_ctx* ctx, int kind, int dtype, size_t bytes) {
+    const xh_config& c = ctx->c;
+    size_t rows = 0, cols = 0;
+    switch (kind) {
+        case XH_EMBED: case XH_WCLS: rows = c.vocab_size; cols = c.dim; break;
+        case XH_ATTN_NORM: case XH_FFN_NORM: case XH_FINAL_NORM: rows = 1; cols = c.dim; break;
+        case XH_WQ: rows = ctx->q_dim; cols = c.dim; break;
+        case XH_WK: case XH_WV: rows = ctx->kv_dim; cols = c.dim; break;
+        case XH_WO: rows = c.dim; cols = ctx->q_dim; break;
+        case XH_W1: case XH_W3: rows = c.hidden_dim; cols = c.dim; break;
+        case XH_W2: rows = c.dim; cols = c.hidden_dim; break;
+        default: return set_err(ctx, XH_E_INVALID, "unknown tensor kind %d", kind);
+    }
+    const size_t esz = dtype_size(dtype);
+    if (esz == 0 || bytes != rows * cols * esz)
+        return set_err(ctx, XH_E_INVALID, "tensor kind %d: %zu bytes, expected %zu ([%zu,%zu] of dtype %d)", kind,
+                       bytes, rows * cols * esz, rows, cols, dtype);
+    return 0;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1157,30 +1189,52 @@ int xh_upload(xh_ctx* ctx, int kind, int layer, int dtype, const void* host, siz
     if (!ctx || !host) return set_err(ctx, XH_E_INVALID, "null argument");
     HIP_TRY(ctx, hipSetDevice(ctx->dev));
     Slot s;
-    // validate the byte count before touching the device layout
-    {
-        const xh_config& c = ctx->c;
-        size_t rows = 0, cols = 0;
-        switch (kind) {
-            case XH_EMBED: case XH_WCLS: rows = c.vocab_size; cols = c.dim; break;
-            case XH_ATTN_NORM: case XH_FFN_NORM: case XH_FINAL_NORM: rows = 1; cols = c.dim; break;
-            case XH_WQ: rows = ctx->q_dim; cols = c.dim; break;
-            case XH_WK: case XH_WV: rows = ctx->kv_dim; cols = c.dim; break;
-            case XH_WO: rows = c.dim; cols = ctx->q_dim; break;
-            case XH_W1: case XH_W3: rows = c.hidden_dim; cols = c.dim; break;
-            case XH_W2: rows = c.dim; cols = c.hidden_dim; break;
-            default: return set_err(ctx, XH_E_INVALID, "unknown tensor kind %d", kind);
-        }
-        const size_t esz = dtype_size(dtype);
-        if (esz == 0 || bytes != rows * cols * esz)
-            return set_err(ctx, XH_E_INVALID, "tensor kind %d: %zu bytes, expected %zu ([%zu,%zu] of dtype %d)", kind,
-                           bytes, rows * cols * esz, rows, cols, dtype);
-    }
-    int rc = tensor_slot(ctx, kind, layer, dtype, &s);
+    int rc = check_bytes(ctx, kind, dtype, bytes);
+    if (!rc) rc = tensor_slot(ctx, kind, layer, dtype, &s);
     if (rc) return rc;
     HIP_TRY(ctx, hipMemcpy2D(s.base, s.pitch, host, s.cols * dtype_size(dtype), s.cols * dtype_size(dtype), s.rows,
                              hipMemcpyHostToDevice));
     return scan_f8(ctx, kind, layer, dtype, s);
+}
+
+// Tensor bytes straight from a file (the .xalm layout: tensor data at an absolute, 32-B
+// aligned offset, convert.py:248-321) into the device slot.  The range is mapped with
+// MAP_POPULATE (read ahead in one pass), registered with the runtime for the duration of
+// the copy and moved by one DMA: no host copy of the tensor.  Measured on MI355X with the
+// file in the page cache (tools/load_bench.py): 45 GB/s, against 16 GB/s for pread into
+// two pinned staging buffers and 33 GB/s for a pageable copy of the mapping.
+int xh_upload_file(xh_ctx* ctx, int kind, int layer, int dtype, const char* path, uint64_t offset, size_t bytes) {
+    if (!ctx || !path) return set_err(ctx, XH_E_INVALID, "null argument");
+    HIP_TRY(ctx, hipSetDevice(ctx->dev));
+    int rc = check_bytes(ctx, kind, dtype, bytes);
+    if (rc) return rc;
+    const int fd = open(path, O_RDONLY | O_CLOEXEC);
+    if (fd < 0) return set_err(ctx, XH_E_INVALID, "%s: %s", path, strerror(errno));
+    struct stat st;
+    if (fstat(fd, &st) != 0 || offset > (uint64_t)st.st_size || bytes > (uint64_t)st.st_size - offset) {
+        close(fd);
+        return set_err(ctx, XH_E_INVALID, "%s: %zu bytes at offset %llu run past the end of the file", path, bytes,
+                       (unsigned long long)offset);
+    }
+    const uint64_t a0 = offset & ~(uint64_t)(sysconf(_SC_PAGESIZE) - 1);
+    const size_t len = bytes + (size_t)(offset - a0);
+    void* map = mmap(nullptr, len, PROT_READ, MAP_SHARED | MAP_POPULATE, fd, (off_t)a0);
+    const int map_errno = errno;
+    close(fd);
+    if (map == MAP_FAILED) return set_err(ctx, XH_E_INVALID, "%s: mmap: %s", path, strerror(map_errno));
+    Slot s;
+    rc = tensor_slot(ctx, kind, layer, dtype, &s);
+    if (!rc) {
+        const size_t row_bytes = s.cols * dtype_size(dtype);
+        // unregistered (e.g. a mapping the driver cannot pin) the same copy runs pageable
+        const bool reg = hipHostRegister(map, len, hipHostRegisterReadOnly) == hipSuccess;
+        const hipError_t e = hipMemcpy2D(s.base, s.pitch, (const char*)map + (offset - a0), row_bytes, row_bytes,
+                                         s.rows, hipMemcpyHostToDevice);
+        if (reg) hipHostUnregister(map);
+        if (e != hipSuccess) rc = set_err(ctx, XH_E_HIP, "%s: copy to the device: %s", path, hipGetErrorString(e));
+    }
+    munmap(map, len);
+    return rc ? rc : scan_f8(ctx, kind, layer, dtype, s);
 }
 
 int xh_upload_synthetic(xh_ctx* ctx, int kind, int layer, int dtype, uint64_t seed, float mean, float std) {

@@ -49,7 +49,6 @@ int xalm_load_model(const char* path, int context, int device_ordinal, xh_ctx** 
         xh_ctx* ctx = nullptr;
         if (xh_create(&abi, device_ordinal, &ctx) != 0) throw std::runtime_error(xh_last_error(nullptr));
         try {
-            std::vector<uint8_t> buf;
             for (const auto& kv : f.tensors) {
                 const std::string& name = kv.first;
                 int kind = -1, layer = 0;
@@ -69,9 +68,8 @@ int xalm_load_model(const char* path, int context, int device_ordinal, xh_ctx** 
                         if (rest == names[i]) kind = kinds[i];
                 }
                 if (kind < 0) continue;  // tokenizer.tokens etc.
-                buf.resize(kv.second.size);
-                f.read(kv.second, buf.data());
-                if (xh_upload(ctx, kind, layer, kv.second.type, buf.data(), buf.size()) != 0)
+                if (xh_upload_file(ctx, kind, layer, kv.second.type, f.file_name.c_str(), kv.second.offset,
+                                   kv.second.size) != 0)
                     throw std::runtime_error(name + ": " + xh_last_error(ctx));
             }
         } catch (...) {

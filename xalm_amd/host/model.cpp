@@ -17,7 +17,8 @@ void check(int rc, xh_ctx* ctx, const char* what) {
 }  // namespace
 
 // Model::from_xalm, src/model.cpp:48-118: the same tensor names and shape checks; the weights
-// go to device memory through xh_upload (which copies, so the host buffer is transient).
+// stream from the file into device memory through xh_upload_file (pinned staging, no host
+// Tensor buffers).
 Model Model::from_xalm(const XalmFile& xalm, const int context, const Device device, const int ordinal) {
     if (device != Device::HIP)
         throw std::invalid_argument(
@@ -28,7 +29,6 @@ Model Model::from_xalm(const XalmFile& xalm, const int context, const Device dev
     xh_ctx* ctx = nullptr;
     check(xh_create(&abi, ordinal, &ctx), nullptr, "xh_create");
     Model m(c, ctx);
-    std::vector<uint8_t> buf;
     auto load = [&](const std::string& name, int kind, int layer, std::vector<int> shape) {
         const TensorInfo& ti = xalm.tensors.at(name);
         if (ti.shape != shape) {
@@ -37,9 +37,8 @@ Model Model::from_xalm(const XalmFile& xalm, const int context, const Device dev
             for (int v : shape) b += std::to_string(v) + ",";
             throw std::invalid_argument("shape mismatch for " + name + ": [" + a + "] vs [" + b + "] expected!");
         }
-        buf.resize(ti.size);
-        xalm.read(ti, buf.data());
-        check(xh_upload(ctx, kind, layer, ti.type, buf.data(), buf.size()), ctx, name.c_str());
+        check(xh_upload_file(ctx, kind, layer, ti.type, xalm.file_name.c_str(), ti.offset, ti.size), ctx,
+              name.c_str());
     };
     const int q_dim = c.n_heads * c.head_dim, kv_dim = c.n_kv_heads * c.head_dim;
     load("embed.weight", XH_EMBED, 0, {c.vocab_size, c.dim});

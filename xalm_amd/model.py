@@ -36,32 +36,40 @@ class Model:
 
     # -- construction ----------------------------------------------------------------
     @classmethod
-    def from_xalm(cls, xf: XalmFile, context: int = 0, device: int = 0) -> "Model":
+    def from_xalm(cls, xf: XalmFile, context: int = 0, device: int = 0, direct: bool = True) -> "Model":
+        """`direct`: tensors stream from the file into device memory (xh_upload_file);
+        otherwise each one is read on the host and copied (xh_upload)."""
         cfg = xf.config(context)
         m = cls(cfg, device)
         c = cfg
         shapes = {L.EMBED: (c.vocab_size, c.dim), L.FINAL_NORM: (c.dim,), L.WCLS: (c.vocab_size, c.dim)}
         for kind, name in xf.global_tensors(bool(c.tie_word_embeddings)).items():
-            m._load(xf, kind, 0, name, shapes[kind])
+            m._load(xf, kind, 0, name, shapes[kind], direct)
         q_dim, kv_dim = c.n_heads * c.head_dim, c.n_kv_heads * c.head_dim
         lshapes = {L.ATTN_NORM: (c.dim,), L.FFN_NORM: (c.dim,), L.WQ: (q_dim, c.dim), L.WK: (kv_dim, c.dim),
                    L.WV: (kv_dim, c.dim), L.WO: (c.dim, q_dim), L.W1: (c.hidden_dim, c.dim),
                    L.W2: (c.dim, c.hidden_dim), L.W3: (c.hidden_dim, c.dim)}
         for layer in range(c.n_layers):
             for kind, name in xf.layer_tensors(layer).items():
-                m._load(xf, kind, layer, name, lshapes[kind])
+                m._load(xf, kind, layer, name, lshapes[kind], direct)
         return m
 
-    def _load(self, xf: XalmFile, kind: int, layer: int, name: str, expected_shape):
+    def _load(self, xf: XalmFile, kind: int, layer: int, name: str, expected_shape, direct: bool = True):
         ti = xf.tensors[name]
         if tuple(ti.shape) != tuple(expected_shape):  # src/model.cpp:381-392
             raise ValueError(f"shape mismatch for {name}: {ti.shape} vs {expected_shape} expected!")
-        raw = np.ascontiguousarray(xf.raw(name))
-        self.upload(kind, layer, xf.dtype(name), raw)
+        if direct:
+            self.upload_file(kind, layer, xf.dtype(name), xf.path, ti.offset, ti.size)
+        else:
+            self.upload(kind, layer, xf.dtype(name), np.ascontiguousarray(xf.raw(name)))
 
     def upload(self, kind: int, layer: int, dtype: int, data: np.ndarray):
         data = np.ascontiguousarray(data)
         L.check(L.lib().xh_upload(self._ctx, kind, layer, dtype, L.ptr(data), data.nbytes), self._ctx)
+
+    def upload_file(self, kind: int, layer: int, dtype: int, path: str, offset: int, nbytes: int):
+        L.check(L.lib().xh_upload_file(self._ctx, kind, layer, dtype, str(path).encode(), int(offset), int(nbytes)),
+                self._ctx)
 
     def upload_synthetic(self, kind: int, layer: int, dtype: int, seed: int, mean: float, std: float):
         L.check(L.lib().xh_upload_synthetic(self._ctx, kind, layer, dtype, seed, mean, std), self._ctx)
