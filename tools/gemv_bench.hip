@@ -1,5 +1,6 @@
-// gemv_bench.hip — one-process A/B of gemv launch shapes on the Mistral-7B f16 matrix shapes.
+// gemv_bench.hip — one-process A/B of gemv launch shapes on the Mistral-7B matrix shapes.
 // Build: hipcc -O3 --offload-arch=gfx950 -std=c++17 -o tools/gemv_bench tools/gemv_bench.hip
+//   fp8 e4m3 weights: add -DGB_DT=XH_F8_E4M3 (-o tools/gemv_bench_f8)
 // Each shape rotates over enough weight copies (> 1 GB) that the 256 MB Infinity Cache
 // cannot serve repeats; variants are interleaved over rounds (guide §5.4 rule 24).
 #include <hip/hip_runtime.h>
@@ -15,11 +16,21 @@
 
 using namespace xalm;
 
+#ifndef GB_DT
+#define GB_DT XH_F16
+#endif
+constexpr int DT = GB_DT;
+constexpr int ESZ = DT == XH_F16 ? 2 : 1;
+
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s @%d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
 
 __global__ void fill(uint16_t* p, size_t n, uint64_t seed) {
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
         p[i] = xs_to_f16(xs_value(seed, i, 0.f, 0.02f));
+}
+__global__ void fill8(uint8_t* p, size_t n, uint64_t seed) {  // e4m3 bytes, no NaN code
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+        p[i] = (uint8_t)(xs_to_f16(xs_value(seed, i, 0.f, 1.f)) >> 3) & 0xF7;
 }
 __global__ void fillf(float* p, size_t n, uint64_t seed) {
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
@@ -30,9 +41,9 @@ struct Mat { const char* name; int rows, n, pro, epi; };
 
 template <int PRO, int EPI, class S>
 void launch(const GemvArgs& a, int max_waves) {
-    const size_t smem = gemv_smem_bytes<XH_F16, S>(a.n);
+    const size_t smem = gemv_smem_bytes<DT, S>(a.n);
     const int blocks = gemv_blocks<S>(a.rows, max_waves / S::WAVES);
-    auto k = gemv_kernel<XH_F16, PRO, EPI, S>;
+    auto k = gemv_kernel<DT, PRO, EPI, S>;
     static bool once = false;
     if (!once) { CK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024)); once = true; }
     hipLaunchKernelGGL(k, dim3(blocks), dim3(S::THREADS), smem, 0, a);
@@ -64,27 +75,36 @@ int main(int argc, char** argv) {
     std::vector<std::vector<uint16_t*>> copies(mats.size());
     for (size_t i = 0; i < mats.size(); i++) {
         const size_t elems = (size_t)mats[i].rows * mats[i].n;
-        const int nc = std::max<int>(2, (int)((1400ull << 20) / (elems * 2)) + 1);
+        const int nc = std::max<int>(2, (int)((1400ull << 20) / (elems * ESZ)) + 1);
         for (int c = 0; c < nc; c++) {
             uint16_t* p;
-            CK(hipMalloc(&p, elems * 2));
-            hipLaunchKernelGGL(fill, dim3(2048), dim3(256), 0, 0, p, elems, 100 + i * 10 + c);
+            CK(hipMalloc(&p, elems * ESZ));
+            if (ESZ == 2) hipLaunchKernelGGL(fill, dim3(2048), dim3(256), 0, 0, p, elems, 100 + i * 10 + c);
+            else hipLaunchKernelGGL(fill8, dim3(2048), dim3(256), 0, 0, (uint8_t*)p, elems, 100 + i * 10 + c);
             copies[i].push_back(p);
         }
     }
     CK(hipDeviceSynchronize());
 
 #define V(NAME, MW, ...) {NAME, [](const Mat& m, const GemvArgs& a) { launch_any<GemvShape<__VA_ARGS__>>(m, a, MW); }}
-    std::vector<Variant> vs = {
+    // PF shapes as the product picks them: x in 2 float4 per thread for n <= 4096, else 8
+#define VPF(NAME, MW, T, R, U) {NAME, [](const Mat& m, const GemvArgs& a) { \
+        if (m.n <= 4096) launch_any<GemvShape<T, R, U, true, 4, true, 2>>(m, a, MW); \
+        else launch_any<GemvShape<T, R, U, true, 4, true, 8>>(m, a, MW); }}
+    std::vector<Variant> vs = DT != XH_F16 ? std::vector<Variant>{
+        VPF("t512 r2 u4 pf (product)", 4096, 512, 2, 4),
+        VPF("t512 r4 u4 pf", 4096, 512, 4, 4),
+        VPF("t512 r2 u4 pf w8192", 8192, 512, 2, 4),
+        VPF("t512 r4 u2 pf", 4096, 512, 4, 2),
+        V("t512 r2 u4 nt --  w4096", 4096, 512, 2, 4, true, 4, false),
+        V("t512 r4 u4 nt --  w4096", 4096, 512, 4, 4, true, 4, false),
+    } : std::vector<Variant>{
         V("t512 r2 u4 nt --  w4096", 4096, 512, 2, 4, true, 4, false),
         V("t512 r1 u8 nt --  w4096", 4096, 512, 1, 8, true, 4, false),
-        V("t512 r1 u8 nt pf  w4096", 4096, 512, 1, 8, true, 4, true),
-        V("t512 r1 u4 nt pf  w4096", 4096, 512, 1, 4, true, 4, true),
+        VPF("t512 r2 u4 pf (product)", 4096, 512, 2, 4),
         V("t512 r2 u8 nt --  w4096", 4096, 512, 2, 8, true, 4, false),
-        V("t512 r2 u4 nt pf  w4096", 4096, 512, 2, 4, true, 4, true),
         V("t256 r1 u8 nt --  w4096", 4096, 256, 1, 8, true, 4, false),
         V("t512 r1 u16 nt -- w2048 mw2", 2048, 512, 1, 16, true, 2, false),
-        V("t512 r2 u8 nt pf  w2048 mw2", 2048, 512, 2, 8, true, 2, true),
     };
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
@@ -97,7 +117,7 @@ int main(int argc, char** argv) {
                 const Mat& m = mats[mi];
                 if (m.n > 8192 && std::string(vs[vi].name).find("t128") == 0) continue;
                 GemvArgs a{};
-                a.row_bytes = (size_t)m.n * 2; a.n = m.n; a.rows = m.rows; a.x = x; a.norm_w = nw;
+                a.row_bytes = (size_t)m.n * ESZ; a.n = m.n; a.rows = m.rows; a.x = x; a.norm_w = nw;
                 a.norm_dtype = XH_F32; a.eps = 1e-5f; a.out = out; a.act = XH_ACT_SILU;
                 for (int i = 0; i < 2; i++) { a.w = copies[mi][i % copies[mi].size()]; vs[vi].fn(m, a); }
                 CK(hipEventRecord(e0, 0));
@@ -110,7 +130,7 @@ int main(int argc, char** argv) {
                 res[mi][vi].push_back(ms * 1000.f / iters);
             }
     for (size_t mi = 0; mi < mats.size(); mi++) {
-        const double bytes = (double)mats[mi].rows * mats[mi].n * 2;
+        const double bytes = (double)mats[mi].rows * mats[mi].n * ESZ;
         printf("%s  (%.1f MB)\n", mats[mi].name, bytes / 1e6);
         for (size_t vi = 0; vi < vs.size(); vi++) {
             auto v = res[mi][vi];
