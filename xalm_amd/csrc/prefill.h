@@ -7,7 +7,7 @@
 // stay f32 exactly as in the reference; only the summation order differs.
 //
 // GEMM layout: Y[t][r] = sum_k X[t][k] W[r][k], W row-major [rows][K] as uploaded.  One wave
-// owns 32 rows x one K slice x up to 64 tokens (two 32x32 f32 accumulator tiles).  Lane l
+// owns RT 32-row tiles x one K slice x up to 64 tokens (2 RT 32x32 f32 accumulators).  Lane l
 // streams 16 bytes of row r0 + (l & 31) at k = kb + E (l >> 5) and decodes them to E floats:
 // they are the B operand of E MFMAs whose A operand is X[t][same k] (MFMA 32x32x2 f32 operand
 // map: A[i = l & 31][k = l >> 5], B[k = l >> 5][j = l & 31]), so weights go HBM -> VGPR ->
@@ -40,35 +40,41 @@ struct PfGemmArgs {
     float* part;       // [ks][n][rows]
 };
 
-// PIPE: K slice a multiple of 4 chunk pairs (weights requested 4 pairs ahead)
-template <int DT, bool PIPE>
+// PIPE: K slice a multiple of 4 chunk pairs (weights requested 4 pairs ahead).  RT: 32-row
+// tiles per wave; each X operand load feeds RT x 2 accumulator tiles.
+template <int DT, bool PIPE, int RT>
 __global__ __launch_bounds__(PF_THREADS) void prefill_gemm_kernel(const PfGemmArgs a) {
     constexpr int E = WDec<DT>::E;
     constexpr int ESZ = 16 / E;  // bytes per element
     const int lane = threadIdx.x & 63;
     const int gw = blockIdx.x * PF_WAVES + (threadIdx.x >> 6);
-    const int n_rt = (a.rows + 31) / 32;
+    const int n_rt = (a.rows + 32 * RT - 1) / (32 * RT);
     if (gw >= n_rt * a.ks) return;
     const int rt = gw / a.ks, s = gw - rt * a.ks;
     const int j = lane & 31, h = lane >> 5;
-    const int r = rt * 32 + j;
     const int kslice = a.K / a.ks;
     const int k0 = s * kslice, k1 = k0 + kslice;
-    const char* wrow = (const char*)a.w + (size_t)min(r, a.rows - 1) * a.row_bytes;
+    const char* wrow[RT];
+#pragma unroll
+    for (int i = 0; i < RT; i++)
+        wrow[i] = (const char*)a.w + (size_t)min((rt * RT + i) * 32 + j, a.rows - 1) * a.row_bytes;
     const int n_tt = (a.n + 31) / 32;
     // token rows of this lane's A operand in each tile (clamped: rows past n are not stored)
     const float* x0 = a.x + (size_t)min(j, a.n - 1) * a.K;
     const float* x1 = a.x + (size_t)min(32 + j, a.n - 1) * a.K;
-    f32x16 acc0 = {}, acc1 = {};
+    f32x16 acc0[RT], acc1[RT];
+#pragma unroll
+    for (int i = 0; i < RT; i++) acc0[i] = acc1[i] = f32x16{};
     // software pipeline over chunk pairs: (weights, X) of later pairs in flight while this
-    // one's 2E MFMAs run (weights come from HBM, X from L2)
+    // one's 2 E RT MFMAs run (weights come from HBM, X from L2)
     struct Stage {
-        u32x4 w;
+        u32x4 w[RT];
         float4 x0[E / 4], x1[E / 4];
     };
     auto load = [&](Stage& st, const int kb) {
         const int k = kb + E * h;
-        st.w = *(const u32x4*)(wrow + (size_t)k * ESZ);
+#pragma unroll
+        for (int i = 0; i < RT; i++) st.w[i] = *(const u32x4*)(wrow[i] + (size_t)k * ESZ);
 #pragma unroll
         for (int q = 0; q < E / 4; q++) st.x0[q] = *(const float4*)(x0 + k + 4 * q);
         if (n_tt > 1) {
@@ -77,22 +83,25 @@ __global__ __launch_bounds__(PF_THREADS) void prefill_gemm_kernel(const PfGemmAr
         }
     };
     auto mfma = [&](const Stage& st) {
-        float wf[E];
-        WDec<DT>::dec(st.w, wf);
 #pragma unroll
-        for (int q = 0; q < E / 4; q++) {
-            acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(st.x0[q].x, wf[4 * q + 0], acc0, 0, 0, 0);
-            acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(st.x0[q].y, wf[4 * q + 1], acc0, 0, 0, 0);
-            acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(st.x0[q].z, wf[4 * q + 2], acc0, 0, 0, 0);
-            acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(st.x0[q].w, wf[4 * q + 3], acc0, 0, 0, 0);
-        }
-        if (n_tt > 1) {
+        for (int i = 0; i < RT; i++) {
+            float wf[E];
+            WDec<DT>::dec(st.w[i], wf);
 #pragma unroll
             for (int q = 0; q < E / 4; q++) {
-                acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(st.x1[q].x, wf[4 * q + 0], acc1, 0, 0, 0);
-                acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(st.x1[q].y, wf[4 * q + 1], acc1, 0, 0, 0);
-                acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(st.x1[q].z, wf[4 * q + 2], acc1, 0, 0, 0);
-                acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(st.x1[q].w, wf[4 * q + 3], acc1, 0, 0, 0);
+                acc0[i] = __builtin_amdgcn_mfma_f32_32x32x2f32(st.x0[q].x, wf[4 * q + 0], acc0[i], 0, 0, 0);
+                acc0[i] = __builtin_amdgcn_mfma_f32_32x32x2f32(st.x0[q].y, wf[4 * q + 1], acc0[i], 0, 0, 0);
+                acc0[i] = __builtin_amdgcn_mfma_f32_32x32x2f32(st.x0[q].z, wf[4 * q + 2], acc0[i], 0, 0, 0);
+                acc0[i] = __builtin_amdgcn_mfma_f32_32x32x2f32(st.x0[q].w, wf[4 * q + 3], acc0[i], 0, 0, 0);
+            }
+            if (n_tt > 1) {
+#pragma unroll
+                for (int q = 0; q < E / 4; q++) {
+                    acc1[i] = __builtin_amdgcn_mfma_f32_32x32x2f32(st.x1[q].x, wf[4 * q + 0], acc1[i], 0, 0, 0);
+                    acc1[i] = __builtin_amdgcn_mfma_f32_32x32x2f32(st.x1[q].y, wf[4 * q + 1], acc1[i], 0, 0, 0);
+                    acc1[i] = __builtin_amdgcn_mfma_f32_32x32x2f32(st.x1[q].z, wf[4 * q + 2], acc1[i], 0, 0, 0);
+                    acc1[i] = __builtin_amdgcn_mfma_f32_32x32x2f32(st.x1[q].w, wf[4 * q + 3], acc1[i], 0, 0, 0);
+                }
             }
         }
     };
@@ -130,14 +139,18 @@ __global__ __launch_bounds__(PF_THREADS) void prefill_gemm_kernel(const PfGemmAr
         }
         if (kb < k1) mfma(sa);  // odd count of chunk pairs: the last one, loaded above
     }
-    if (r >= a.rows) return;
     // D map: column j = lane & 31 (row r), row i = (reg & 3) + 8 (reg >> 2) + 4 h (token)
-    float* out = a.part + (size_t)s * a.n * a.rows + r;
 #pragma unroll
-    for (int reg = 0; reg < 16; reg++) {
-        const int t = (reg & 3) + 8 * (reg >> 2) + 4 * h;
-        if (t < a.n) out[(size_t)t * a.rows] = acc0[reg];
-        if (n_tt > 1 && 32 + t < a.n) out[(size_t)(32 + t) * a.rows] = acc1[reg];
+    for (int i = 0; i < RT; i++) {
+        const int r = (rt * RT + i) * 32 + j;
+        if (r >= a.rows) continue;
+        float* out = a.part + (size_t)s * a.n * a.rows + r;
+#pragma unroll
+        for (int reg = 0; reg < 16; reg++) {
+            const int t = (reg & 3) + 8 * (reg >> 2) + 4 * h;
+            if (t < a.n) out[(size_t)t * a.rows] = acc0[i][reg];
+            if (n_tt > 1 && 32 + t < a.n) out[(size_t)(32 + t) * a.rows] = acc1[i][reg];
+        }
     }
 }
 

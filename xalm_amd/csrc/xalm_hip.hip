@@ -659,8 +659,9 @@ int host_step_params(xh_ctx* ctx, int token, int pos) {
 // ---------------------------------------------------------------------------------------
 template <class T>
 int dmalloc(xh_ctx* ctx, T** p, size_t n);
-constexpr int PF_WAVE_TARGET = 2048;  // 2 waves per SIMD (4096 measured slower: more split-K partials)
-constexpr size_t PF_PART_ROWS = 32 * PF_WAVE_TARGET;  // >= ks * rows of every GEMM (ks * ceil(rows/32) <= target)
+constexpr int PF_WAVE_TARGET = 1024;  // 1 wave per SIMD (RT=2: 2048 -16 %, 512 -38 %; fewer, longer K slices)
+constexpr int PF_RT = 2;                // 32-row tiles per GEMM wave (1: -11 %, 4: -9 %)
+constexpr size_t PF_PART_ROWS = 32 * PF_RT * PF_WAVE_TARGET;  // >= ks * rows (ks * ceil(rows/(32 RT)) <= target)
 
 int pf_alloc(xh_ctx* ctx) {
     if (ctx->pf_alloc) return 0;
@@ -683,7 +684,7 @@ int pf_alloc(xh_ctx* ctx) {
 // K slices for a GEMM of `rows` outputs: about PF_WAVE_TARGET waves, K divisible into whole
 // chunk pairs
 int pf_ks(int rows, int K, int E) {
-    const int n_rt = (rows + 31) / 32;
+    const int n_rt = (rows + 32 * PF_RT - 1) / (32 * PF_RT);
     int ks = 1;
     // slices stay whole multiples of 4 chunk pairs (the pipelined kernel) where K allows
     const int unit = K % (8 * E) == 0 ? 8 * E : 2 * E;
@@ -693,13 +694,13 @@ int pf_ks(int rows, int K, int E) {
 
 template <int DT>
 void pf_gemm_t(const PfGemmArgs& a, hipStream_t s) {
-    const int waves = (a.rows + 31) / 32 * a.ks;
+    const int waves = (a.rows + 32 * PF_RT - 1) / (32 * PF_RT) * a.ks;
     constexpr int E = WDec<DT>::E;
     const dim3 grid((waves + PF_WAVES - 1) / PF_WAVES);
     if ((a.K / a.ks) % (8 * E) == 0)
-        hipLaunchKernelGGL((prefill_gemm_kernel<DT, true>), grid, dim3(PF_THREADS), 0, s, a);
+        hipLaunchKernelGGL((prefill_gemm_kernel<DT, true, PF_RT>), grid, dim3(PF_THREADS), 0, s, a);
     else
-        hipLaunchKernelGGL((prefill_gemm_kernel<DT, false>), grid, dim3(PF_THREADS), 0, s, a);
+        hipLaunchKernelGGL((prefill_gemm_kernel<DT, false, PF_RT>), grid, dim3(PF_THREADS), 0, s, a);
 }
 // Y partials of W[rows][K] . X[n][K]; returns ks (0: dtype / shape not supported)
 int pf_gemm(xh_ctx* ctx, int dt, const void* w, int K, int rows, const float* x, int n) {
