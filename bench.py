@@ -254,6 +254,15 @@ def main():
                    "mode": "batched" if model.get_option(L.OPT_PREFILL) else "per-token",
                    "note": "passes of 64 tokens; every matrix product on v_mfma_f32_32x32x2_f32 (f32 activations, "
                            "as the reference); f32 MFMA peak 157 TF/s", "matmul_tflops": round(flops / pf_s / 1e12, 1)}
+        # run_perplexity's loop (xh_perplexity): the same tokens, every token's logits and
+        # sample_prob of the next one on the device
+        t0 = time.perf_counter()
+        probs = model.token_probs(ptoks, 0)
+        sync_all(None, torch_mod)
+        pp_s = time.perf_counter() - t0
+        prefill["perplexity"] = {"tokens": len(ptoks) - 1, "ms": round(pp_s * 1e3, 2),
+                                 "tok_s": round((len(ptoks) - 1) / pp_s, 1),
+                                 "finite": bool(np.isfinite(np.log(probs)).all())}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not w["kv_prefill"]:

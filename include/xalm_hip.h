@@ -137,6 +137,14 @@ int xh_decode_greedy(xh_ctx* ctx, int pos, int n_steps, int stop_token_a, int st
  * (src/main.cpp:94-100) in one call.  logits_out may be NULL. */
 int xh_prefill(xh_ctx* ctx, const int* tokens, int n, int pos0, int want_logits, float* logits_out);
 
+/* Perplexity scoring, the loop of run_perplexity (src/main.cpp:243-254) in one call: forward
+ * tokens[0..n-1) at positions pos0.. with logits and write probs_out[i] =
+ * Sampler::sample_prob(tokens[i+1]) (src/sampler.cpp:3-17; n-1 floats, caller-owned).  The
+ * logits stay on the device; with XH_OPT_PREFILL on, passes of 64 tokens compute every
+ * token's logits with one lm_head GEMM.  n >= 2.  The caller takes log and sums, as the
+ * reference does in double. */
+int xh_perplexity(xh_ctx* ctx, const int* tokens, int n, int pos0, float* probs_out);
+
 /* Device engine: 0 = one hipGraph of kernels per token (gemv / attention launches);
  * 1 = the persistent decode kernel (one launch per call, every phase inside, weights
  * streamed ahead across the hand-offs; needs one dtype for all layer matrices and norms and

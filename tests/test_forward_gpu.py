@@ -276,6 +276,60 @@ def test_upload_validation():
         gm.forward(st, 1, 0)  # weights missing
 
 
+def check_probs(got, om, toks):
+    """got[i] vs the oracle's Sampler::sample_prob(toks[i+1]) after forwarding toks[i] (the
+    run_perplexity loop, src/main.cpp:243-254).  Bar: |log p - log p_ref| <= 2 x the logits
+    bar of that position (log p moves by at most twice the worst logit error); probabilities
+    the reference underflows to 0 (|logits| ~ 87 on small_llama) must be below 1e-30 here."""
+    assert got.shape == (len(toks) - 1,)
+    for pos in range(len(toks) - 1):
+        om.forward(toks[pos], pos)
+        lg = om.logits()
+        ref = O.sample_prob(lg, toks[pos + 1])
+        if ref < 1e-30:
+            assert got[pos] < 1e-30, (pos, got[pos], ref)
+            continue
+        assert got[pos] > 0, (pos, got[pos], ref)
+        err = abs(np.log(got[pos]) - np.log(ref))
+        assert err <= 2 * tol(lg) + 1e-5, (pos, got[pos], ref, err)
+
+
+@pytest.mark.parametrize("prefill", [1, 0])
+@pytest.mark.parametrize("name", ["tiny_mistral_f16", "tiny_mistral_bf16", "tiny_mistral_f8_e4m3",
+                                  "small_llama_f16"])
+def test_perplexity_probs_match_oracle(name, prefill):
+    # xh_perplexity: batched passes (prefill 1: 89 tokens = a full 64-token pass + 25, lm_head
+    # as one GEMM per pass) and the token loop (prefill 0)
+    xf = XalmFile(fixture_path(name + ".xalm"))
+    gm = Model.from_xalm(xf, context=256)
+    gm.set_option(L.OPT_PREFILL, prefill)
+    om = O.OracleModel.from_xalm(xf, context=256)
+    toks = [1] + [3 + (i * 41) % 280 for i in range(89)]
+    check_probs(gm.token_probs(toks), om, toks)
+
+
+@pytest.mark.parametrize("case", ["persistent", "ring"])
+def test_perplexity_token_loop_paths(case):
+    # the persistent engine, and a sequence longer than -T (ring wrap + sinks): token by token
+    xf = XalmFile(fixture_path("tiny_mistral_f16.xalm"))
+    ctxlen = 16 if case == "ring" else 0
+    gm = Model.from_xalm(xf, context=ctxlen)
+    if case == "persistent":
+        gm.set_engine(1)
+    om = O.OracleModel.from_xalm(xf, context=ctxlen)
+    toks = [1] + [3 + (i * 23) % 290 for i in range(40)]
+    check_probs(gm.token_probs(toks), om, toks)
+
+
+def test_perplexity_arguments():
+    xf = XalmFile(fixture_path("tiny_mistral_f16.xalm"))
+    gm = Model.from_xalm(xf)
+    with pytest.raises(L.XhError):
+        gm.token_probs([1])  # needs a target
+    with pytest.raises(L.XhError):
+        gm.token_probs([1, 10 ** 6])  # target out of range
+
+
 @pytest.mark.parametrize("name", FIXTURES)
 def test_upload_file_equals_host_upload(name):
     # xh_upload_file (pread into pinned staging + DMA) and xh_upload (host buffer) must leave

@@ -59,6 +59,7 @@ _SIGNATURES = {
     "xh_forward": (_I, [_P, _I, _I, _I, _P]),
     "xh_decode_greedy": (_I, [_P, _I, _I, _I, _I, _P, ctypes.POINTER(_I)]),
     "xh_prefill": (_I, [_P, _P, _I, _I, _I, _P]),
+    "xh_perplexity": (_I, [_P, _P, _I, _I, _P]),
     "xh_set_engine": (_I, [_P, _I]),
     "xh_get_engine": (_I, [_P]),
     "xh_last_launch_us": (_I, [_P, _FP]),

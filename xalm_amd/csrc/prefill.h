@@ -159,7 +159,8 @@ struct PfEpiArgs {
     const float* part;  // [ks][n][rows]
     int ks, n, rows;
     int epi;            // EPI_QKV / EPI_RESID / EPI_GLU / EPI_STORE
-    float* out;         // RESID: X [n][rows] (+=); GLU: H [n][rows/2]; STORE: [n][rows]
+    float* out;         // RESID: X [n][rows] (+=); GLU: H [n][rows/2]; STORE: [n][out_stride]
+    size_t out_stride;  // STORE row stride (0: rows)
     // EPI_QKV
     float* q;           // [n][q_dim]
     uint16_t* kcache;   // this layer's rings [max_seq_len][kv_dim]
@@ -172,25 +173,27 @@ struct PfEpiArgs {
 };
 
 __global__ __launch_bounds__(256) void prefill_epi_kernel(const PfEpiArgs a) {
-    // one thread per output pair (rows are even for QKV / GLU; RESID / STORE take both)
-    const int pairs = a.rows / 2;
+    // one thread per output pair (rows are even for QKV / GLU / RESID; STORE may be odd: the
+    // last pair's second row is not written)
+    const int pairs = (a.rows + 1) / 2;
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= a.n * pairs) return;
     const int t = idx / pairs, r = 2 * (idx - t * pairs);
     float v0 = 0.f, v1 = 0.f;
+    const bool two = r + 1 < a.rows;
     for (int s = 0; s < a.ks; s++) {  // slice order: fixed
         const float* p = a.part + ((size_t)s * a.n + t) * a.rows + r;
         v0 += p[0];
-        v1 += p[1];
+        if (two) v1 += p[1];
     }
     if (a.epi == EPI_RESID) {
         float* o = a.out + (size_t)t * a.rows + r;
         o[0] += v0;
         o[1] += v1;
     } else if (a.epi == EPI_STORE) {
-        float* o = a.out + (size_t)t * a.rows + r;
+        float* o = a.out + (size_t)t * (a.out_stride ? a.out_stride : a.rows) + r;
         o[0] = v0;
-        o[1] = v1;
+        if (r + 1 < a.rows) o[1] = v1;
     } else if (a.epi == EPI_GLU) {
         a.out[(size_t)t * (a.rows / 2) + r / 2] = act_fn(a.act, v0) * v1;
     } else {  // EPI_QKV: src/infer.cpp:392-414 at pos = pos0 + t

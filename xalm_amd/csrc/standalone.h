@@ -102,4 +102,36 @@ __global__ __launch_bounds__(1024) void logits_cand_kernel(const float* logits, 
     cand[tid] = tid == 0 ? bb : 0ull;
 }
 
+// Sampler::sample_prob (src/sampler.cpp:3-17) of one logits row per workgroup: max over the
+// row starting at FLT_MIN (the reference's quirk: a row of logits all below it is shifted by
+// FLT_MIN, not by its own max), then expf(l[target] - max) / sum_i expf(l[i] - max).  The sum
+// is a tree, not the reference's index-ordered loop: float rounding differs, nothing else.
+// Row t: logits + t * stride; probs[t] = the probability of targets[t].
+__global__ __launch_bounds__(1024) void token_prob_kernel(const float* logits, int vocab, size_t stride,
+                                                          const int* targets, float* probs) {
+    __shared__ float red[16];
+    const float* l = logits + (size_t)blockIdx.x * stride;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    float m = FLT_MIN;
+    for (int i = tid; i < vocab; i += 1024) m = l[i] > m ? l[i] : m;  // NaN never wins, as `>`
+    m = wave_max(m);
+    if (lane == 0) red[wid] = m;
+    __syncthreads();
+    m = red[0];
+#pragma unroll
+    for (int w = 1; w < 16; w++) m = red[w] > m ? red[w] : m;
+    __syncthreads();
+    float s = 0.f;
+    for (int i = tid; i < vocab; i += 1024) s += expf(l[i] - m);
+    s = wave_sum(s);
+    if (lane == 0) red[wid] = s;
+    __syncthreads();
+    if (tid == 0) {
+        float tot = 0.f;
+#pragma unroll
+        for (int w = 0; w < 16; w++) tot += red[w];
+        probs[blockIdx.x] = expf(l[targets[blockIdx.x]] - m) / tot;
+    }
+}
+
 }  // namespace xalm

@@ -124,6 +124,12 @@ struct xh_ctx {
     StepParams* pf_sp = nullptr;                 // [PF_TOK] per-token attention scalars
     float *pf_po = nullptr, *pf_pml = nullptr;   // [PF_TOK][nsplit][q_dim], [PF_TOK][nsplit][n_heads][2]
     int* pf_cnt = nullptr;                       // [PF_TOK][n_kv_heads] split tickets
+    // xh_perplexity: per-token logits of a pass, targets, probabilities (allocated on first use)
+    float* pf_logits = nullptr;                  // [PF_TOK][vocab]
+    int* pf_tgt = nullptr;                       // [PF_TOK]
+    int* ppl_tgt = nullptr;                      // [ppl_cap] targets (per-token path)
+    float* ppl_prob = nullptr;                   // [ppl_cap]
+    int ppl_cap = 0;
     int t_max_aw = 16;
     bool use_graphs = true;
     hipGraphExec_t g_logits = nullptr, g_hydrate = nullptr, g_decode = nullptr;
@@ -727,7 +733,7 @@ int pf_gemm(xh_ctx* ctx, int dt, const void* w, int K, int rows, const float* x,
 }
 void pf_epi(xh_ctx* ctx, PfEpiArgs e) {
     e.part = ctx->pf_part;
-    const int threads = e.n * (e.rows / 2);
+    const int threads = e.n * ((e.rows + 1) / 2);
     hipLaunchKernelGGL(prefill_epi_kernel, dim3((threads + 255) / 256), dim3(256), 0, ctx->stream, e);
 }
 template <int HD, int QPK>
@@ -764,11 +770,19 @@ bool pf_supported(const xh_ctx* ctx, int n, int pos0) {
     return c.dim % 32 == 0 && c.hidden_dim % 32 == 0 && ctx->q_dim % 32 == 0;
 }
 
-// tokens[0..n) at positions pos0..: HYDRATE for every token, then the last token's logits
-int prefill_batched(xh_ctx* ctx, const int* tokens, int n, int pos0, int want_logits) {
+constexpr int PF_CLS_CHUNK = (int)(PF_PART_ROWS / 4);  // lm_head rows per GEMM (ks <= 4 fits the partials)
+
+// tokens[0..n) at positions pos0..: HYDRATE for every token, then the last token's logits.
+// probs (device, n floats) != nullptr: also every token's logits (final rmsnorm + lm_head as
+// one GEMM per pass) and probs[i] = sample_prob(targets[i]) (targets: host, n ints).
+int prefill_batched(xh_ctx* ctx, const int* tokens, int n, int pos0, int want_logits, const int* targets = nullptr,
+                    float* probs = nullptr) {
     const xh_config& c = ctx->c;
     int rc = pf_alloc(ctx);
     if (rc) return rc;
+    if (probs && !ctx->pf_logits &&
+        ((rc = dmalloc(ctx, &ctx->pf_logits, (size_t)PF_TOK * c.vocab_size)) || (rc = dmalloc(ctx, &ctx->pf_tgt, (size_t)PF_TOK))))
+        return rc;
     std::vector<StepParams> sps(PF_TOK);
     for (int off = 0; off < n; off += PF_TOK) {
         const int m = std::min(n - off, PF_TOK);
@@ -825,6 +839,27 @@ int prefill_batched(xh_ctx* ctx, const int* tokens, int n, int pos0, int want_lo
             e = PfEpiArgs{};
             e.ks = ks; e.n = m; e.rows = c.dim; e.epi = EPI_RESID; e.out = ctx->pf_x;
             pf_epi(ctx, e);
+        }
+        if (probs) {
+            // Model::forward's OUTPUT_LOGITS tail (src/infer.cpp:620-637) for every token of the
+            // pass, then Sampler::sample_prob of each token's target
+            HIP_TRY(ctx, hipMemcpyAsync(ctx->pf_tgt, targets + off, (size_t)m * sizeof(int), hipMemcpyHostToDevice,
+                                        ctx->stream));
+            hipLaunchKernelGGL(prefill_rmsnorm_kernel, dim3(m), dim3(256), 0, ctx->stream, (const float*)ctx->pf_x, c.dim,
+                               (const void*)ctx->final_norm, ctx->final_norm_dt, c.norm_eps, ctx->pf_xn);
+            const size_t cls_rb = (size_t)c.dim * dtype_size(ctx->wcls_dt);
+            for (int r0 = 0; r0 < c.vocab_size; r0 += PF_CLS_CHUNK) {
+                const int rows = std::min(PF_CLS_CHUNK, c.vocab_size - r0);
+                const int ks = pf_gemm(ctx, kdt(ctx->wcls_dt, ctx->wcls_x), (const char*)ctx->wcls + (size_t)r0 * cls_rb,
+                                       c.dim, rows, ctx->pf_xn, m);
+                if (!ks) return set_err(ctx, XH_E_INVALID, "perplexity: lm_head shape not supported");
+                PfEpiArgs e{};
+                e.ks = ks; e.n = m; e.rows = rows; e.epi = EPI_STORE; e.out = ctx->pf_logits + r0;
+                e.out_stride = (size_t)c.vocab_size;
+                pf_epi(ctx, e);
+            }
+            hipLaunchKernelGGL(token_prob_kernel, dim3(m), dim3(1024), 0, ctx->stream, (const float*)ctx->pf_logits,
+                               c.vocab_size, (size_t)c.vocab_size, (const int*)ctx->pf_tgt, probs + off);
         }
         HIP_TRY(ctx, hipGetLastError());
         if (off + m == n) {
@@ -1004,6 +1039,7 @@ void xh_destroy(xh_ctx* ctx) {
     hipFree(ctx->kv); hipFree(ctx->x); hipFree(ctx->q); hipFree(ctx->attn_out); hipFree(ctx->hb);
     hipFree(ctx->logits); hipFree(ctx->part_o); hipFree(ctx->part_ml); hipFree(ctx->attn_cnt); hipFree(ctx->aw_sync); hipFree(ctx->qaw_sync); hipFree(ctx->cand); hipFree(ctx->scan_flag);
     hipFree(ctx->pf_tok); hipFree(ctx->pf_x); hipFree(ctx->pf_xn); hipFree(ctx->pf_q); hipFree(ctx->pf_att); hipFree(ctx->pf_h);
+    hipFree(ctx->pf_logits); hipFree(ctx->pf_tgt); hipFree(ctx->ppl_tgt); hipFree(ctx->ppl_prob);
     hipFree(ctx->pf_part); hipFree(ctx->pf_sp); hipFree(ctx->pf_po); hipFree(ctx->pf_pml); hipFree(ctx->pf_cnt); hipFree(ctx->rope_freq);
     hipFree(ctx->pk_layers); hipFree(ctx->pk_counters); hipFree(ctx->pk_tickets); hipFree(ctx->pk_err);
     hipFree(ctx->pk_cand); hipFree(ctx->pk_prompt); hipFree(ctx->pk_trace);
@@ -1439,6 +1475,48 @@ int xh_prefill(xh_ctx* ctx, const int* tokens, int n, int pos0, int want_logits,
     if (logits_out && want_logits)
         HIP_TRY(ctx, hipMemcpyAsync(logits_out, ctx->logits, (size_t)ctx->c.vocab_size * 4, hipMemcpyDeviceToHost,
                                     ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    return check_aw(ctx);
+}
+
+// The perplexity loop of run_perplexity (src/main.cpp:243-254): forward tokens[0..n-1) at
+// positions pos0.. with logits, probs_out[i] = Sampler::sample_prob(tokens[i + 1]) after token
+// i (src/sampler.cpp:3-17).  The logits never leave the device; batched passes where the
+// prompt path allows, else token by token.
+int xh_perplexity(xh_ctx* ctx, const int* tokens, int n, int pos0, float* probs_out) {
+    if (!ctx || !tokens || !probs_out || n < 2 || pos0 < 0) return set_err(ctx, XH_E_INVALID, "bad perplexity arguments");
+    for (int i = 0; i < n; i++)
+        if (tokens[i] < 0 || tokens[i] >= ctx->c.vocab_size) return set_err(ctx, XH_E_INVALID, "token out of range");
+    HIP_TRY(ctx, hipSetDevice(ctx->dev));
+    int rc = check_ready(ctx);
+    if (rc) return rc;
+    const int m = n - 1, V = ctx->c.vocab_size;
+    if (ctx->ppl_cap < m) {
+        hipFree(ctx->ppl_tgt); hipFree(ctx->ppl_prob);
+        ctx->ppl_tgt = nullptr; ctx->ppl_prob = nullptr; ctx->ppl_cap = 0;
+        if ((rc = dmalloc(ctx, &ctx->ppl_tgt, (size_t)m)) || (rc = dmalloc(ctx, &ctx->ppl_prob, (size_t)m))) return rc;
+        ctx->ppl_cap = m;
+    }
+    if (!use_persistent(ctx) && pf_supported(ctx, m, pos0)) {
+        rc = prefill_batched(ctx, tokens, m, pos0, 0, tokens + 1, ctx->ppl_prob);
+    } else {
+        HIP_TRY(ctx, hipMemcpy(ctx->ppl_tgt, tokens + 1, (size_t)m * sizeof(int), hipMemcpyHostToDevice));
+        for (int i = 0; i < m && !rc; i++) {
+            if (use_persistent(ctx)) {
+                rc = run_persistent(ctx, tokens + i, 1, 0, pos0 + i, 1, -1, -1, nullptr);
+            } else {
+                rc = host_step_params(ctx, tokens[i], pos0 + i);
+                if (!rc) rc = run_step(ctx, true);
+            }
+            if (rc) break;
+            hipLaunchKernelGGL(token_prob_kernel, dim3(1), dim3(1024), 0, ctx->stream, (const float*)ctx->logits, V,
+                               (size_t)V, (const int*)ctx->ppl_tgt + i, ctx->ppl_prob + i);
+            // the step parameters are copied from one pinned host slot: drain before reuse
+            if (hipStreamSynchronize(ctx->stream) != hipSuccess) rc = set_err(ctx, XH_E_HIP, "hipStreamSynchronize failed");
+        }
+    }
+    if (rc) return rc;
+    HIP_TRY(ctx, hipMemcpyAsync(probs_out, ctx->ppl_prob, (size_t)m * sizeof(float), hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     return check_aw(ctx);
 }

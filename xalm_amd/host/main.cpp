@@ -102,16 +102,17 @@ static void run_perplexity(const std::string& path, Device dev, const std::strin
     const XalmFile file = XalmFile::load(path);
     const Model model = Model::from_xalm(file, context, dev);
     InferenceState state(model.config);
-    const Sampler sampler(model.config);
     const Tokenizer tokenizer(file);
     model.forward(state, 0, 0);
     const std::vector<int> encoding = tokenizer.encode(prompt, true);
     double sum_logprob = 0.0, ss_logprob = 0.0;
     const size_t N = encoding.size() - 1;
     const auto t0 = clk::now();
-    for (size_t pos = 0; pos + 1 < encoding.size(); pos++) {
-        model.forward(state, encoding[pos], (int)pos);
-        const double logprob = std::log(sampler.sample_prob(encoding[pos + 1], state));
+    // the forward + sample_prob loop runs on the device (logits never cross to the host); the
+    // log and the double sums stay here, as in the reference
+    const std::vector<float> probs = model.token_probs(encoding, 0);
+    for (size_t pos = 0; pos < N; pos++) {
+        const double logprob = std::log(probs[pos]);
         sum_logprob += logprob;
         ss_logprob += logprob * logprob;
     }

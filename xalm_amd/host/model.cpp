@@ -17,7 +17,7 @@ void check(int rc, xh_ctx* ctx, const char* what) {
 }  // namespace
 
 // Model::from_xalm, src/model.cpp:48-118: the same tensor names and shape checks; the weights
-// stream from the file into device memory through xh_upload_file (pinned staging, no host
+// stream from the file into device memory through xh_upload_file (mapped, pinned and DMAd; no host
 // Tensor buffers).
 Model Model::from_xalm(const XalmFile& xalm, const int context, const Device device, const int ordinal) {
     if (device != Device::HIP)
@@ -81,6 +81,13 @@ std::vector<int> Model::decode_greedy(const int pos, const int n_steps, const in
     check(xh_decode_greedy(_ctx, pos, n_steps, stop_a, stop_b, toks.data(), &done), _ctx, "xh_decode_greedy");
     toks.resize((size_t)done);
     return toks;
+}
+
+std::vector<float> Model::token_probs(const std::vector<int>& tokens, const int pos0) const {
+    if (tokens.size() < 2) return {};
+    std::vector<float> p(tokens.size() - 1);
+    check(xh_perplexity(_ctx, tokens.data(), (int)tokens.size(), pos0, p.data()), _ctx, "xh_perplexity");
+    return p;
 }
 
 void Model::fetch_logits(InferenceState& s) const { check(xh_get_logits(_ctx, s.logits()), _ctx, "xh_get_logits"); }

@@ -97,6 +97,9 @@ public:
     // greedy decode on the device (no host round trip per token); returns the tokens
     std::vector<int> decode_greedy(int pos, int n_steps, int stop_a = -1, int stop_b = -1) const;
     void fetch_logits(InferenceState& s) const;
+    // run_perplexity's loop on the device (xh_perplexity): element i = Sampler::sample_prob of
+    // tokens[i + 1] after forwarding tokens[i] at pos0 + i
+    std::vector<float> token_probs(const std::vector<int>& tokens, int pos0) const;
     [[nodiscard]] size_t active_bytes(size_t pos) const;
     xh_ctx* ctx() const { return _ctx; }
 

@@ -97,6 +97,14 @@ class Model:
         L.check(L.lib().xh_prefill(self._ctx, L.ptr(toks), int(toks.size), int(pos0), int(s is not None), out),
                 self._ctx)
 
+    def token_probs(self, tokens, pos0: int = 0) -> np.ndarray:
+        """run_perplexity's loop (src/main.cpp:243-254) on the device: forward tokens[:-1] at
+        positions pos0.., element i = Sampler::sample_prob(tokens[i + 1]) after token i."""
+        toks = np.ascontiguousarray(np.asarray(tokens, dtype=np.int32))
+        out = np.zeros(max(toks.size - 1, 1), dtype=np.float32)
+        L.check(L.lib().xh_perplexity(self._ctx, L.ptr(toks), int(toks.size), int(pos0), L.ptr(out)), self._ctx)
+        return out[: toks.size - 1]
+
     # engine: 0 = hipGraph of kernels per token, 1 = persistent kernel, -1 = automatic
     ENGINE_GRAPH, ENGINE_PERSISTENT, ENGINE_AUTO = 0, 1, -1
 
