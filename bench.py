@@ -114,6 +114,28 @@ def sync_all(dist, torch_mod):
         dist.barrier()
 
 
+def timed_region(dist, torch_mod, fn):
+    """fn() bracketed by a barrier + device sync on both sides; returns (fn's result, the MAX
+    over ranks of the wall time), so every rank reports the slowest replica's time."""
+    sync_all(dist, torch_mod)
+    t0 = time.perf_counter()
+    out = fn()
+    sync_all(dist, torch_mod)
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        dist.barrier()
+    return out, elapsed
+
+
+def job_value(world, steps, elapsed):
+    """whole-job decode throughput: every replica decodes `steps` tokens (weak scaling)"""
+    return world * steps / elapsed
+
+
 def cpu_baseline(w, c, prompt, gpu_logits0, gpu_tokens, n_decode):
     """Oracle (restated src/infer.cpp, OpenMP) on the same weights, bounded sample."""
     from oracle import oracle as O
@@ -205,19 +227,8 @@ def main():
     if pos + args.steps > c.max_seq_len and not w["kv_prefill"]:
         raise SystemExit(f"steps exceed the {c.max_seq_len} context")
 
-    sync_all(dist, torch_mod)
-    t0 = time.perf_counter()
-    toks = model.decode_greedy(pos, args.steps)
-    sync_all(dist, torch_mod)
-    t1 = time.perf_counter()
-    elapsed = t1 - t0
+    toks, elapsed = timed_region(dist, torch_mod, lambda: model.decode_greedy(pos, args.steps))
     launch_us = model.last_launch_us() if engine == 1 else None
-    if dist is not None:
-        import torch
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        dist.barrier()
     assert len(toks) == args.steps
 
     # algorithmic bytes of the timed tokens: Model::active_bytes(pos) (src/model.cpp:12-35)
@@ -286,7 +297,7 @@ def main():
                     "traffic_source": src,
                     "kernel": "gemv_kernel<PRO_RMSNORM,EPI_GLU> (fused W1/W3 + rmsnorm + silu*up), layer 0",
                     "bytes_per_launch": k_bytes, "avg_launch_us": round(k_us, 2)}
-    value = world * args.steps / elapsed
+    value = job_value(world, args.steps, elapsed)
     if rank == 0:
         out = {
             "metric": "decode tok/s + %HBM-roofline, Mistral-7B fp16, 1xMI355X vs -d cpu",

@@ -214,7 +214,8 @@ __global__ __launch_bounds__(AW_THREADS) void attn_wo_kernel(const AttnArgs aa, 
                 for (int r = 0; r < S::ROWS; r++) xres[r] = g * S::ROWS + r < ga.rows ? ga.out[g * S::ROWS + r] : 0.f;
             }
         };
-        const bool early = wid != 0 && !(ga.act & 256);
+        // waves 1.. request their Wo rows before the hand-off; wave 0 polls the flag first
+        const bool early = wid != 0;
         if (g < n_groups && early) fetch();
         wait_heads();
         if (g < n_groups && !early) fetch();

@@ -386,8 +386,7 @@ bool use_attn_wo(const xh_ctx* ctx, int l) {
 
 int launch_attn_wo(xh_ctx* ctx, int l, hipStream_t s) {
     const AttnArgs aa = attn_args(ctx, l);
-    GemvArgs ga = wo_args(ctx, l);
-    if (getenv("XH_AW_NOPF")) ga.act |= 256;  // experiment: Wo loads after the hand-off
+    const GemvArgs ga = wo_args(ctx, l);
     unsigned* sync = ctx->aw_sync + (size_t)AW_SYNC_WORDS * l;
     const int hd = ctx->c.head_dim, qpk = ctx->qpk, nkv = ctx->c.n_kv_heads, tm = ctx->t_max_aw;
     const int mw = ctx->max_gemv_waves;
