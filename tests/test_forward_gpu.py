@@ -145,15 +145,19 @@ def test_prefill_matches_oracle(name, context, engine):
         assert np.abs(a - b).max() <= 2e-3 * max(1.0, np.abs(b).max())
 
 
+@pytest.mark.parametrize("mode", [1, 2])
 @pytest.mark.parametrize("name", FIXTURES)
 @pytest.mark.parametrize("n", [1, 37, 64, 150])
-def test_batched_prefill_matches_oracle(name, n):
-    """xh_prefill's batched path (prefill.h: f32-MFMA GEMMs over passes of <= 64 tokens,
-    causal attention per token) vs the oracle's token-by-token HYDRATE loop: last logits,
-    every layer's K and V rows, and the greedy continuation after it."""
+def test_batched_prefill_matches_oracle(name, n, mode):
+    """xh_prefill's batched path (prefill.h: MFMA GEMMs over passes of <= 64 tokens, causal
+    attention per token) vs the oracle's token-by-token HYDRATE loop: last logits, every
+    layer's K and V rows, and the greedy continuation after it.  mode 1: f32-input MFMA;
+    mode 2: split-f16 MFMA (f16 / fp8 weights; other dtypes keep the f32 kernel)."""
     xf = XalmFile(fixture_path(name + ".xalm"))
     gm = Model.from_xalm(xf, context=256)
     assert gm.get_option(L.OPT_PREFILL) == 1
+    gm.set_option(L.OPT_PREFILL, mode)
+    assert gm.get_option(L.OPT_PREFILL) == mode
     om = O.OracleModel.from_xalm(xf, context=256)
     toks = [1] + [3 + (i * 37) % 280 for i in range(n - 1)]
     st = InferenceState(gm.config)
@@ -173,12 +177,58 @@ def test_batched_prefill_matches_oracle(name, n):
     assert np.abs(st.logits() - om.logits()).max() <= tol(om.logits())
 
 
-def test_batched_prefill_equals_token_loop():
+def synthetic_pair(wdt, dim=256, hidden=512, n_layers=2, vocab=512, context=256):
+    """The same synthetic weights (include/xalm_synth.h) in a device Model and the oracle."""
+    cfg = L.XhConfig()
+    cfg.dim, cfg.hidden_dim, cfg.head_dim, cfg.n_layers = dim, hidden, 64, n_layers
+    cfg.n_heads, cfg.n_kv_heads, cfg.vocab_size, cfg.max_seq_len = 4, 1, vocab, context
+    cfg.rope_theta, cfg.rotary_dim, cfg.norm_eps, cfg.act = 1e6, 64, 1e-5, L.ACT_SILU
+    cfg.qkv_clip, cfg.tie_word_embeddings = float(np.finfo(np.float32).max), 0
+    gm, om = Model(cfg), O.OracleModel(cfg)
+    q_dim, kv_dim = cfg.n_heads * cfg.head_dim, cfg.n_kv_heads * cfg.head_dim
+    shape = {L.EMBED: (vocab, dim), L.WCLS: (vocab, dim), L.FINAL_NORM: (1, dim), L.ATTN_NORM: (1, dim),
+             L.FFN_NORM: (1, dim), L.WQ: (q_dim, dim), L.WK: (kv_dim, dim), L.WV: (kv_dim, dim),
+             L.WO: (dim, q_dim), L.W1: (hidden, dim), L.W2: (dim, hidden), L.W3: (hidden, dim)}
+    specs = [(L.EMBED, 0, L.F16, 11, 0.0, 1.0), (L.WCLS, 0, L.F16, 12, 0.0, 0.05),
+             (L.FINAL_NORM, 0, L.BF16, 13, 1.0, 0.01)]
+    for layer in range(n_layers):
+        for i, kind in enumerate([L.WQ, L.WK, L.WV, L.WO, L.W1, L.W2, L.W3]):
+            specs.append((kind, layer, wdt, 100 + 10 * layer + i, 0.0, 0.05))
+        specs += [(L.ATTN_NORM, layer, L.BF16, 300 + layer, 1.0, 0.01), (L.FFN_NORM, layer, L.BF16, 400 + layer, 1.0, 0.01)]
+    for kind, layer, dt, seed, mean, std in specs:
+        gm.upload_synthetic(kind, layer, dt, seed, mean, std)
+        rows, cols = shape[kind]
+        om.set_tensor(kind, layer, dt, O.synthetic(rows, cols, dt, seed, mean, std))
+    return gm, om
+
+
+@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("wdt", [L.F16, L.F8_E4M3, L.F8_E5M2])
+def test_prefill_gemm_paths_on_synthetic_weights(wdt, mode):
+    # dims (256 / 512) that take the split-f16 kernel for fp8 too (K % 8E); 100 tokens = a full
+    # pass and a partial one; logits vs the oracle's token loop, then the perplexity path
+    gm, om = synthetic_pair(wdt)
+    gm.set_option(L.OPT_PREFILL, mode)
+    toks = [1] + [3 + (i * 37) % 500 for i in range(99)]
+    st = InferenceState(gm.config)
+    gm.prefill(toks, 0, st)
+    for pos, tok in enumerate(toks):
+        om.forward(tok, pos, L.OUTPUT_LOGITS if pos == len(toks) - 1 else L.HYDRATE_KV_CACHE)
+    ref = om.logits()
+    assert np.isfinite(st.logits()).all()
+    assert np.abs(st.logits() - ref).max() <= tol(ref), float(np.abs(st.logits() - ref).max())
+    gm2, om2 = synthetic_pair(wdt)
+    gm2.set_option(L.OPT_PREFILL, mode)
+    check_probs(gm2.token_probs(toks[:70]), om2, toks[:70])
+
+
+@pytest.mark.parametrize("batched", [1, 2])
+def test_batched_prefill_equals_token_loop(batched):
     """Batched and per-token prefill of the same prompt agree (logits and K/V rings)."""
     xf = XalmFile(fixture_path("small_llama_f16.xalm"))
     toks = [1] + [3 + (i * 53) % 300 for i in range(99)]
     out = []
-    for mode in (1, 0):
+    for mode in (batched, 0):
         gm = Model.from_xalm(xf, context=512)
         gm.set_option(L.OPT_PREFILL, mode)
         st = InferenceState(gm.config)
@@ -294,7 +344,7 @@ def check_probs(got, om, toks):
         assert err <= 2 * tol(lg) + 1e-5, (pos, got[pos], ref, err)
 
 
-@pytest.mark.parametrize("prefill", [1, 0])
+@pytest.mark.parametrize("prefill", [1, 2, 0])
 @pytest.mark.parametrize("name", ["tiny_mistral_f16", "tiny_mistral_bf16", "tiny_mistral_f8_e4m3",
                                   "small_llama_f16"])
 def test_perplexity_probs_match_oracle(name, prefill):

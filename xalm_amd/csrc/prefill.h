@@ -154,6 +154,172 @@ __global__ __launch_bounds__(PF_THREADS) void prefill_gemm_kernel(const PfGemmAr
     }
 }
 
+// ---- split-f16 GEMM (XH_OPT_PREFILL 2) ----------------------------------------------------
+// Y = X W^T on v_mfma_f32_32x32x16_f16 (8x the K of the f32 MFMA per instruction, half its
+// cycles).  Each activation row is scaled by a power of two s_t (row max in [2^14, 2^15)) and
+// split exactly-as-possible into two f16: hi = f16(s x), lo = f16(s x - hi), |x - (hi+lo)/s|
+// <= 2^-22 |x| (below f16's subnormal floor: 2^-38 of the row max).  Products are exact
+// (f16 x f16 in f32) and accumulate in f32; the store multiplies by 1/s_t (exact).  Weights
+// must convert exactly to f16: f16 itself, e4m3 (via f32), e5m2 (its code is an f16's top
+// byte); bf16 / f32 / Q8 / NaN-holding fp8 take the f32-MFMA kernel.
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+
+// one workgroup per token row: s_t, hi, lo (row-major [n][K] f16), inv_s[t] = 1 / s_t
+__global__ __launch_bounds__(256) void prefill_split_kernel(const float* x, int K, uint16_t* xh, uint16_t* xl,
+                                                            float* inv_s) {
+    __shared__ float red[4];
+    const float* xr = x + (size_t)blockIdx.x * K;
+    float m = 0.f;
+    for (int i = threadIdx.x; i < K; i += 256) m = fmaxf(m, fabsf(xr[i]));
+    m = wave_max(m);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+    __syncthreads();
+    m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    // m = f 2^e with f in [0.5, 1): s = 2^(15 - e) puts s m in [2^14, 2^15); a zero or
+    // non-finite row keeps s = 1
+    int e = 0;
+    const bool ok = m > 0.f && m <= FLT_MAX;
+    if (ok) frexpf(m, &e);  // m = f * 2^e, f in [0.5, 1)
+    const float s = ok ? ldexpf(1.f, 15 - e) : 1.f;
+    for (int i = threadIdx.x; i < K; i += 256) {
+        const float v = xr[i] * s;
+        const _Float16 hi = (_Float16)v;
+        const _Float16 lo = (_Float16)(v - (float)hi);
+        xh[(size_t)blockIdx.x * K + i] = __builtin_bit_cast(uint16_t, hi);
+        xl[(size_t)blockIdx.x * K + i] = __builtin_bit_cast(uint16_t, lo);
+    }
+    if (threadIdx.x == 0) inv_s[blockIdx.x] = 1.f / s;
+}
+
+// 16 weight bytes -> E/8 B operands of 8 f16 (k order = byte order)
+template <int DT>
+__device__ __forceinline__ void w_f16(const u32x4 w, f16x8* b) {
+    if constexpr (DT == XH_F16) {
+        b[0] = __builtin_bit_cast(f16x8, w);
+    } else if constexpr (DT == XH_F8_E5M2) {
+        const uint32_t u[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+        for (int e = 0; e < 16; e++)  // code c -> f16 bits c << 8
+            b[e >> 3][e & 7] = __builtin_bit_cast(_Float16, (uint16_t)(((u[e >> 2] >> (8 * (e & 3))) & 0xffu) << 8));
+    } else {
+        static_assert(DT == XH_F8_E4M3, "split-f16 GEMM: weights must convert exactly to f16");
+        float f[16];
+        WDec<DT>::dec(w, f);
+#pragma unroll
+        for (int e = 0; e < 16; e++) b[e >> 3][e & 7] = (_Float16)f[e];  // exact: e4m3 fits f16
+    }
+}
+
+struct PfGemm16Args {
+    const void* w;        // [rows][K]
+    size_t row_bytes;
+    int K, rows;
+    const uint16_t* xh;   // [n][K] f16 bits
+    const uint16_t* xl;
+    const float* inv_s;   // [n]
+    int n, ks;
+    float* part;          // [ks][n][rows]
+};
+
+// Lane l of a wave: weight bytes of row (tile i, l & 31) at k = kb + E h (h = l >> 5); MFMA
+// m of the chunk pairs B = 8 of them (k = kb + E h + 8 m + j) with A = X at the same k, so
+// A and B agree on k for every lane (the sum over k is order-free up to f32 rounding).
+template <int DT, int RT>
+__global__ __launch_bounds__(PF_THREADS) void prefill_gemm16_kernel(const PfGemm16Args a) {
+    constexpr int E = WDec<DT>::E;
+    constexpr int ESZ = 16 / E;
+    constexpr int M = E / 8;  // MFMAs per 16 weight bytes
+    const int lane = threadIdx.x & 63;
+    const int gw = blockIdx.x * PF_WAVES + (threadIdx.x >> 6);
+    const int n_rt = (a.rows + 32 * RT - 1) / (32 * RT);
+    if (gw >= n_rt * a.ks) return;
+    const int rt = gw / a.ks, s = gw - rt * a.ks;
+    const int j = lane & 31, h = lane >> 5;
+    const int kslice = a.K / a.ks;
+    const int k0 = s * kslice;
+    const char* wrow[RT];
+#pragma unroll
+    for (int i = 0; i < RT; i++)
+        wrow[i] = (const char*)a.w + (size_t)min((rt * RT + i) * 32 + j, a.rows - 1) * a.row_bytes;
+    const int n_tt = (a.n + 31) / 32;
+    const size_t r0 = (size_t)min(j, a.n - 1) * a.K, r1 = (size_t)min(32 + j, a.n - 1) * a.K;
+    f32x16 acc0[RT], acc1[RT];
+#pragma unroll
+    for (int i = 0; i < RT; i++) acc0[i] = acc1[i] = f32x16{};
+    struct Stage {
+        u32x4 w[RT];
+        u32x4 h0[M], l0[M], h1[M], l1[M];
+    };
+    auto load = [&](Stage& st, const int kb) {
+        const int k = kb + E * h;
+#pragma unroll
+        for (int i = 0; i < RT; i++) st.w[i] = *(const u32x4*)(wrow[i] + (size_t)k * ESZ);
+#pragma unroll
+        for (int m = 0; m < M; m++) {
+            st.h0[m] = *(const u32x4*)(a.xh + r0 + k + 8 * m);
+            st.l0[m] = *(const u32x4*)(a.xl + r0 + k + 8 * m);
+        }
+        if (n_tt > 1) {
+#pragma unroll
+            for (int m = 0; m < M; m++) {
+                st.h1[m] = *(const u32x4*)(a.xh + r1 + k + 8 * m);
+                st.l1[m] = *(const u32x4*)(a.xl + r1 + k + 8 * m);
+            }
+        }
+    };
+    auto mfma = [&](const Stage& st) {
+#pragma unroll
+        for (int i = 0; i < RT; i++) {
+            f16x8 b[M];
+            w_f16<DT>(st.w[i], b);
+#pragma unroll
+            for (int m = 0; m < M; m++) {
+                acc0[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, st.h0[m]), b[m], acc0[i], 0, 0, 0);
+                acc0[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, st.l0[m]), b[m], acc0[i], 0, 0, 0);
+            }
+            if (n_tt > 1) {
+#pragma unroll
+                for (int m = 0; m < M; m++) {
+                    acc1[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, st.h1[m]), b[m], acc1[i], 0, 0, 0);
+                    acc1[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, st.l1[m]), b[m], acc1[i], 0, 0, 0);
+                }
+            }
+        }
+    };
+    // 4-deep ring over chunk pairs (2E k per stage); kslice % (8E) == 0 (host-checked);
+    // clamped indices keep every load unconditional
+    const int P = kslice / (2 * E);
+    auto ld = [&](Stage& st, const int c) { load(st, k0 + 2 * E * min(c, P - 1)); };
+    Stage s0, s1, s2, s3;
+    ld(s0, 0);
+    ld(s1, 1);
+    ld(s2, 2);
+    ld(s3, 3);
+    for (int c = 0; c < P; c += 4) {
+        mfma(s0);
+        ld(s0, c + 4);
+        mfma(s1);
+        ld(s1, c + 5);
+        mfma(s2);
+        ld(s2, c + 6);
+        mfma(s3);
+        ld(s3, c + 7);
+    }
+    // D map: column j = lane & 31 (row r), row i = (reg & 3) + 8 (reg >> 2) + 4 h (token)
+#pragma unroll
+    for (int i = 0; i < RT; i++) {
+        const int r = (rt * RT + i) * 32 + j;
+        if (r >= a.rows) continue;
+        float* out = a.part + (size_t)s * a.n * a.rows + r;
+#pragma unroll
+        for (int reg = 0; reg < 16; reg++) {
+            const int t = (reg & 3) + 8 * (reg >> 2) + 4 * h;
+            if (t < a.n) out[(size_t)t * a.rows] = acc0[i][reg] * a.inv_s[t];
+            if (n_tt > 1 && 32 + t < a.n) out[(size_t)(32 + t) * a.rows] = acc1[i][reg] * a.inv_s[32 + t];
+        }
+    }
+}
+
 // Per-pass token scalars
 struct PfEpiArgs {
     const float* part;  // [ks][n][rows]

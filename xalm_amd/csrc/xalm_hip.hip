@@ -115,7 +115,10 @@ struct xh_ctx {
     bool qaw_ok = true;            // cleared when a launch reports the shape unsupported
     // batched prefill (prefill.h), buffers allocated on first use
     bool prefill_batched = true;
+    bool prefill_f16 = false;                    // XH_OPT_PREFILL 2: split-f16 MFMA GEMMs
     bool pf_alloc = false;
+    uint16_t *pf_xh = nullptr, *pf_xl = nullptr; // [PF_TOK][max K] f16 halves of a GEMM input
+    float* pf_xs = nullptr;                      // [PF_TOK] 1 / row scale
     int* pf_tok = nullptr;                       // [PF_TOK]
     float *pf_x = nullptr, *pf_xn = nullptr;     // [PF_TOK][dim]
     float *pf_q = nullptr, *pf_att = nullptr;    // [PF_TOK][q_dim]
@@ -666,7 +669,8 @@ template <class T>
 int dmalloc(xh_ctx* ctx, T** p, size_t n);
 constexpr int PF_WAVE_TARGET = 1024;  // 1 wave per SIMD (RT=2: 2048 -16 %, 512 -38 %; fewer, longer K slices)
 constexpr int PF_RT = 2;                // 32-row tiles per GEMM wave (1: -11 %, 4: -9 %)
-constexpr size_t PF_PART_ROWS = 32 * PF_RT * PF_WAVE_TARGET;  // >= ks * rows (ks * ceil(rows/(32 RT)) <= target)
+constexpr int PF_RT16 = 4;              // 32-row tiles per split-f16 GEMM wave
+constexpr size_t PF_PART_ROWS = 32 * PF_RT16 * PF_WAVE_TARGET;  // >= ks * rows (ks * ceil(rows/(32 RT)) <= target)
 
 int pf_alloc(xh_ctx* ctx) {
     if (ctx->pf_alloc) return 0;
@@ -681,6 +685,10 @@ int pf_alloc(xh_ctx* ctx) {
         (rc = dmalloc(ctx, &ctx->pf_po, (size_t)PF_TOK * ctx->nsplit * ctx->q_dim)) ||
         (rc = dmalloc(ctx, &ctx->pf_pml, (size_t)PF_TOK * ctx->nsplit * c.n_heads * 2)) ||
         (rc = dmalloc(ctx, &ctx->pf_cnt, (size_t)PF_TOK * c.n_kv_heads)))
+        return rc;
+    const size_t kmax = std::max({(size_t)c.dim, (size_t)c.hidden_dim, (size_t)ctx->q_dim});
+    if ((rc = dmalloc(ctx, &ctx->pf_xh, PF_TOK * kmax)) || (rc = dmalloc(ctx, &ctx->pf_xl, PF_TOK * kmax)) ||
+        (rc = dmalloc(ctx, &ctx->pf_xs, (size_t)PF_TOK)))
         return rc;
     ctx->pf_alloc = true;
     return 0;
@@ -707,8 +715,44 @@ void pf_gemm_t(const PfGemmArgs& a, hipStream_t s) {
     else
         hipLaunchKernelGGL((prefill_gemm_kernel<DT, false, PF_RT>), grid, dim3(PF_THREADS), 0, s, a);
 }
+// split-f16 GEMM: K slices of whole 4-stage rings (8E), about PF_WAVE_TARGET waves, partials fit
+int pf_ks16(int rows, int K, int E) {
+    if (K % (8 * E)) return 0;
+    const int n_rt = (rows + 32 * PF_RT16 - 1) / (32 * PF_RT16);
+    int ks = 1;
+    while (ks < 64 && (size_t)2 * ks * n_rt <= PF_WAVE_TARGET && K % (2 * ks * 8 * E) == 0) ks *= 2;
+    while (ks > 1 && (size_t)ks * rows > PF_PART_ROWS) ks /= 2;
+    return (size_t)ks * rows <= PF_PART_ROWS ? ks : 0;
+}
+template <int DT>
+void pf_gemm16_t(const PfGemm16Args& a, hipStream_t s) {
+    const int waves = (a.rows + 32 * PF_RT16 - 1) / (32 * PF_RT16) * a.ks;
+    hipLaunchKernelGGL((prefill_gemm16_kernel<DT, PF_RT16>), dim3((waves + PF_WAVES - 1) / PF_WAVES), dim3(PF_THREADS),
+                       0, s, a);
+}
+// the split-f16 form of pf_gemm (XH_OPT_PREFILL 2) for weights exact in f16; 0 = not taken
+int pf_gemm16(xh_ctx* ctx, int dt, const void* w, int K, int rows, const float* x, int n) {
+    if (dt != XH_F16 && dt != XH_F8_E4M3 && dt != XH_F8_E5M2) return 0;
+    const int E = elems_per_16b(dt);
+    const int ks = pf_ks16(rows, K, E);
+    if (!ks) return 0;
+    hipLaunchKernelGGL(prefill_split_kernel, dim3(n), dim3(256), 0, ctx->stream, x, K, ctx->pf_xh, ctx->pf_xl, ctx->pf_xs);
+    PfGemm16Args a{};
+    a.w = w; a.row_bytes = (size_t)K * (16 / E); a.K = K; a.rows = rows;
+    a.xh = ctx->pf_xh; a.xl = ctx->pf_xl; a.inv_s = ctx->pf_xs; a.n = n; a.ks = ks; a.part = ctx->pf_part;
+    switch (dt) {
+        case XH_F16: pf_gemm16_t<XH_F16>(a, ctx->stream); break;
+        case XH_F8_E4M3: pf_gemm16_t<XH_F8_E4M3>(a, ctx->stream); break;
+        default: pf_gemm16_t<XH_F8_E5M2>(a, ctx->stream); break;
+    }
+    return ks;
+}
 // Y partials of W[rows][K] . X[n][K]; returns ks (0: dtype / shape not supported)
 int pf_gemm(xh_ctx* ctx, int dt, const void* w, int K, int rows, const float* x, int n) {
+    if (ctx->prefill_f16) {
+        const int ks = pf_gemm16(ctx, dt, w, K, rows, x, n);
+        if (ks) return ks;
+    }
     const int E = (dt == XH_F8_E4M3_EXACT || dt == XH_F8_E5M2_EXACT) ? 16 : elems_per_16b(dt);
     if (K % (2 * E)) return 0;
     PfGemmArgs a{};
@@ -1038,6 +1082,7 @@ void xh_destroy(xh_ctx* ctx) {
     hipFree(ctx->kv); hipFree(ctx->x); hipFree(ctx->q); hipFree(ctx->attn_out); hipFree(ctx->hb);
     hipFree(ctx->logits); hipFree(ctx->part_o); hipFree(ctx->part_ml); hipFree(ctx->attn_cnt); hipFree(ctx->aw_sync); hipFree(ctx->qaw_sync); hipFree(ctx->cand); hipFree(ctx->scan_flag);
     hipFree(ctx->pf_tok); hipFree(ctx->pf_x); hipFree(ctx->pf_xn); hipFree(ctx->pf_q); hipFree(ctx->pf_att); hipFree(ctx->pf_h);
+    hipFree(ctx->pf_xh); hipFree(ctx->pf_xl); hipFree(ctx->pf_xs);
     hipFree(ctx->pf_logits); hipFree(ctx->pf_tgt); hipFree(ctx->ppl_tgt); hipFree(ctx->ppl_prob);
     hipFree(ctx->pf_part); hipFree(ctx->pf_sp); hipFree(ctx->pf_po); hipFree(ctx->pf_pml); hipFree(ctx->pf_cnt); hipFree(ctx->rope_freq);
     hipFree(ctx->pk_layers); hipFree(ctx->pk_counters); hipFree(ctx->pk_tickets); hipFree(ctx->pk_err);
@@ -1563,7 +1608,7 @@ int xh_get_option(const xh_ctx* ctx, int option, int* value) {
             *value = ctx->fuse_level >= 2 && ctx->qaw_ok && aw_instantiated(ctx->c.head_dim, ctx->qpk) ? 2
                      : ctx->fuse_attn_wo ? 1 : 0;
             return 0;
-        case XH_OPT_PREFILL: *value = ctx->prefill_batched ? 1 : 0; return 0;
+        case XH_OPT_PREFILL: *value = !ctx->prefill_batched ? 0 : ctx->prefill_f16 ? 2 : 1; return 0;
         default: return XH_E_INVALID;
     }
 }
@@ -1583,7 +1628,9 @@ int xh_set_option(xh_ctx* ctx, int option, int value) {
             drop_graphs(ctx);
             return 0;
         case XH_OPT_PREFILL:
+            if (value < 0 || value > 2) return set_err(ctx, XH_E_INVALID, "XH_OPT_PREFILL: 0, 1 or 2");
             ctx->prefill_batched = value != 0;
+            ctx->prefill_f16 = value == 2;
             return 0;
         default: return set_err(ctx, XH_E_INVALID, "unknown option %d", option);
     }
