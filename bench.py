@@ -181,8 +181,9 @@ def main():
     ap.add_argument("--kernel-iters", type=int, default=200)
     ap.add_argument("--engine", type=int, default=-1, choices=(-1, 0, 1),
                     help="-1 auto (persistent kernel when instantiated), 0 graph of kernels, 1 persistent")
-    ap.add_argument("--prefill-mode", type=int, default=1, choices=(1, 2),
-                    help="batched prefill GEMMs: 1 f32-input MFMA, 2 split-f16 MFMA (f16 / fp8 weights)")
+    ap.add_argument("--prefill-mode", type=int, default=1, choices=(1, 2, 3),
+                    help="batched prefill GEMMs (XH_OPT_PREFILL): 1 default per dtype, 2 split-f16 MFMA "
+                         "wherever the weights allow, 3 f32-input MFMA only")
     ap.add_argument("--prefill-tokens", type=int, default=512,
                     help="also time xh_prefill of this many prompt tokens (batched f32-MFMA path; 0 = skip)")
     ap.add_argument("--fuse-attn-wo", type=int, default=1, choices=(0, 1, 2),
@@ -265,10 +266,11 @@ def main():
         flops = 2.0 * args.prefill_tokens * c.n_layers * layer_params  # matrix products only
         prefill = {"tokens": args.prefill_tokens, "ms": round(pf_s * 1e3, 2),
                    "tok_s": round(args.prefill_tokens / pf_s, 1),
-                   "mode": {0: "per-token", 1: "batched f32-MFMA", 2: "batched split-f16 MFMA"}[
-                       model.get_option(L.OPT_PREFILL)],
-                   "note": "passes of 64 tokens; every matrix product on v_mfma_f32_32x32x2_f32 (f32 activations, "
-                           "as the reference); f32 MFMA peak 157 TF/s", "matmul_tflops": round(flops / pf_s / 1e12, 1)}
+                   "mode": {0: "per-token", 1: "batched (f32-input MFMA; split-f16 MFMA for fp8 weights)",
+                            2: "batched split-f16 MFMA", 3: "batched f32-input MFMA"}[model.get_option(L.OPT_PREFILL)],
+                   "note": "passes of 64 tokens; f32-input MFMA v_mfma_f32_32x32x2_f32 (f32 activations as the "
+                           "reference, peak 157 TF/s) or v_mfma_f32_32x32x16_f16 on exact f16 hi+lo activation pairs",
+                   "matmul_tflops": round(flops / pf_s / 1e12, 1)}
         # run_perplexity's loop (xh_perplexity): the same tokens, every token's logits and
         # sample_prob of the next one on the device
         t0 = time.perf_counter()

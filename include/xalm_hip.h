@@ -185,9 +185,13 @@ int xh_set_graphs(xh_ctx* ctx, int enable);
  * and Wo (+ residual) in ONE launch with in-launch hand-offs (qaw.h); 1 = qkv launch, then
  * attention + Wo in one launch (attn_wo.h); 0 = three launches.  Same math.  Level 2 falls
  * back to 1 where the shape is not instantiated; xh_get_option reports the level in effect. */
-/* XH_OPT_PREFILL (default 1): xh_prefill processes the prompt in passes of up to 64 tokens,
- * each weight matrix streamed once per pass into f32-input MFMA GEMMs (prefill.h); 0 = one
- * forward per token (the reference's loop, src/main.cpp:94-100).  Same math per token. */
+/* XH_OPT_PREFILL (default 1): xh_prefill / xh_perplexity process the prompt in passes of up to
+ * 64 tokens, each weight matrix streamed once per pass into MFMA GEMMs (prefill.h): 1 = f32-input
+ * MFMA (activations exactly as the reference), except fp8 weights, which take the split-f16
+ * MFMA (activations as exact f16 hi + lo pairs under a power-of-two row scale, ≈22-bit
+ * mantissa; measured faster there); 2 = split-f16 wherever the weights convert exactly to
+ * f16 (f16, fp8); 3 = f32-input MFMA only; 0 = one forward per token (the reference's loop,
+ * src/main.cpp:94-100).  Same math per token up to f32 rounding. */
 enum xh_option { XH_OPT_FUSE_ATTN_WO = 1, XH_OPT_PREFILL = 2 };
 int xh_set_option(xh_ctx* ctx, int option, int value);
 int xh_get_option(const xh_ctx* ctx, int option, int* value);

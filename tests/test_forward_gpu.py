@@ -145,14 +145,14 @@ def test_prefill_matches_oracle(name, context, engine):
         assert np.abs(a - b).max() <= 2e-3 * max(1.0, np.abs(b).max())
 
 
-@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("mode", [1, 2, 3])
 @pytest.mark.parametrize("name", FIXTURES)
 @pytest.mark.parametrize("n", [1, 37, 64, 150])
 def test_batched_prefill_matches_oracle(name, n, mode):
     """xh_prefill's batched path (prefill.h: MFMA GEMMs over passes of <= 64 tokens, causal
     attention per token) vs the oracle's token-by-token HYDRATE loop: last logits, every
-    layer's K and V rows, and the greedy continuation after it.  mode 1: f32-input MFMA;
-    mode 2: split-f16 MFMA (f16 / fp8 weights; other dtypes keep the f32 kernel)."""
+    layer's K and V rows, and the greedy continuation after it.  mode 1: the default choice
+    per dtype; 2: split-f16 MFMA wherever the weights allow (f16 / fp8); 3: f32-input MFMA."""
     xf = XalmFile(fixture_path(name + ".xalm"))
     gm = Model.from_xalm(xf, context=256)
     assert gm.get_option(L.OPT_PREFILL) == 1
@@ -202,7 +202,7 @@ def synthetic_pair(wdt, dim=256, hidden=512, n_layers=2, vocab=512, context=256)
     return gm, om
 
 
-@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("mode", [1, 2, 3])
 @pytest.mark.parametrize("wdt", [L.F16, L.F8_E4M3, L.F8_E5M2])
 def test_prefill_gemm_paths_on_synthetic_weights(wdt, mode):
     # dims (256 / 512) that take the split-f16 kernel for fp8 too (K % 8E); 100 tokens = a full
@@ -222,7 +222,7 @@ def test_prefill_gemm_paths_on_synthetic_weights(wdt, mode):
     check_probs(gm2.token_probs(toks[:70]), om2, toks[:70])
 
 
-@pytest.mark.parametrize("batched", [1, 2])
+@pytest.mark.parametrize("batched", [1, 2, 3])
 def test_batched_prefill_equals_token_loop(batched):
     """Batched and per-token prefill of the same prompt agree (logits and K/V rings)."""
     xf = XalmFile(fixture_path("small_llama_f16.xalm"))
@@ -344,7 +344,7 @@ def check_probs(got, om, toks):
         assert err <= 2 * tol(lg) + 1e-5, (pos, got[pos], ref, err)
 
 
-@pytest.mark.parametrize("prefill", [1, 2, 0])
+@pytest.mark.parametrize("prefill", [1, 2, 3, 0])
 @pytest.mark.parametrize("name", ["tiny_mistral_f16", "tiny_mistral_bf16", "tiny_mistral_f8_e4m3",
                                   "small_llama_f16"])
 def test_perplexity_probs_match_oracle(name, prefill):

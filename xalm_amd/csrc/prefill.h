@@ -164,11 +164,32 @@ __global__ __launch_bounds__(PF_THREADS) void prefill_gemm_kernel(const PfGemmAr
 // byte); bf16 / f32 / Q8 / NaN-holding fp8 take the f32-MFMA kernel.
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
-// one workgroup per token row: s_t, hi, lo (row-major [n][K] f16), inv_s[t] = 1 / s_t
-__global__ __launch_bounds__(256) void prefill_split_kernel(const float* x, int K, uint16_t* xh, uint16_t* xl,
-                                                            float* inv_s) {
+// A-operand fragment layout of X for weights with E elements per 16 bytes (M = E / 8 MFMAs per
+// chunk): block (token tile tt, chunk c of 2E k, m) holds 64 x 16 bytes, lane l's 8 f16 at
+// 16 l = X[32 tt + (l & 31)][2E c + E (l >> 5) + 8 m + j], so a wave's fragment load is one
+// contiguous 1 KB read (a row-major gather touches 32 rows per load and saturated L1).
+__host__ __device__ inline size_t frag_off(const int tt, const int c, const int m, const int lane, const int n_c,
+                                           const int M) {
+    return ((((size_t)tt * n_c + c) * M + m) * 64 + lane) * 8;  // in f16 elements
+}
+
+// one workgroup per token row (grid = 32 x token tiles; rows past n are zero): s_t, hi, lo in
+// the fragment layout, inv_s[t] = 1 / s_t
+__global__ __launch_bounds__(256) void prefill_split_kernel(const float* x, int K, int n, int E, uint16_t* xh,
+                                                            uint16_t* xl, float* inv_s) {
     __shared__ float red[4];
-    const float* xr = x + (size_t)blockIdx.x * K;
+    const int t = blockIdx.x;
+    const int M = E / 8, n_c = K / (2 * E);
+    if (t >= n) {
+        for (int i = threadIdx.x; i < K / 8; i += 256) {
+            const int k = 8 * i, c = k / (2 * E), r = k - c * 2 * E, hh = r / E, m = (r - hh * E) / 8;
+            const size_t o = frag_off(t >> 5, c, m, (t & 31) + 32 * hh, n_c, M);
+            *(u32x4*)(xh + o) = u32x4{0u, 0u, 0u, 0u};
+            *(u32x4*)(xl + o) = u32x4{0u, 0u, 0u, 0u};
+        }
+        return;
+    }
+    const float* xr = x + (size_t)t * K;
     float m = 0.f;
     for (int i = threadIdx.x; i < K; i += 256) m = fmaxf(m, fabsf(xr[i]));
     m = wave_max(m);
@@ -181,14 +202,21 @@ __global__ __launch_bounds__(256) void prefill_split_kernel(const float* x, int 
     const bool ok = m > 0.f && m <= FLT_MAX;
     if (ok) frexpf(m, &e);  // m = f * 2^e, f in [0.5, 1)
     const float s = ok ? ldexpf(1.f, 15 - e) : 1.f;
-    for (int i = threadIdx.x; i < K; i += 256) {
-        const float v = xr[i] * s;
-        const _Float16 hi = (_Float16)v;
-        const _Float16 lo = (_Float16)(v - (float)hi);
-        xh[(size_t)blockIdx.x * K + i] = __builtin_bit_cast(uint16_t, hi);
-        xl[(size_t)blockIdx.x * K + i] = __builtin_bit_cast(uint16_t, lo);
+    for (int i = threadIdx.x; i < K / 8; i += 256) {
+        const int k = 8 * i, c = k / (2 * E), r = k - c * 2 * E, hh = r / E, mm = (r - hh * E) / 8;
+        const float4 a = *(const float4*)(xr + k), b = *(const float4*)(xr + k + 4);
+        const float v[8] = {a.x * s, a.y * s, a.z * s, a.w * s, b.x * s, b.y * s, b.z * s, b.w * s};
+        f16x8 hi, lo;
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            hi[j] = (_Float16)v[j];
+            lo[j] = (_Float16)(v[j] - (float)hi[j]);
+        }
+        const size_t o = frag_off(t >> 5, c, mm, (t & 31) + 32 * hh, n_c, M);
+        *(f16x8*)(xh + o) = hi;
+        *(f16x8*)(xl + o) = lo;
     }
-    if (threadIdx.x == 0) inv_s[blockIdx.x] = 1.f / s;
+    if (threadIdx.x == 0) inv_s[t] = 1.f / s;
 }
 
 // 16 weight bytes -> E/8 B operands of 8 f16 (k order = byte order)
@@ -242,7 +270,7 @@ __global__ __launch_bounds__(PF_THREADS) void prefill_gemm16_kernel(const PfGemm
     for (int i = 0; i < RT; i++)
         wrow[i] = (const char*)a.w + (size_t)min((rt * RT + i) * 32 + j, a.rows - 1) * a.row_bytes;
     const int n_tt = (a.n + 31) / 32;
-    const size_t r0 = (size_t)min(j, a.n - 1) * a.K, r1 = (size_t)min(32 + j, a.n - 1) * a.K;
+    const int n_c = a.K / (2 * E);
     f32x16 acc0[RT], acc1[RT];
 #pragma unroll
     for (int i = 0; i < RT; i++) acc0[i] = acc1[i] = f32x16{};
@@ -250,20 +278,21 @@ __global__ __launch_bounds__(PF_THREADS) void prefill_gemm16_kernel(const PfGemm
         u32x4 w[RT];
         u32x4 h0[M], l0[M], h1[M], l1[M];
     };
-    auto load = [&](Stage& st, const int kb) {
-        const int k = kb + E * h;
+    // chunk c: weights at k = 2E c + E h; X fragments of token tiles 0 / 1 (prefill_split_kernel)
+    auto load = [&](Stage& st, const int c) {
+        const int k = 2 * E * c + E * h;
 #pragma unroll
         for (int i = 0; i < RT; i++) st.w[i] = *(const u32x4*)(wrow[i] + (size_t)k * ESZ);
 #pragma unroll
         for (int m = 0; m < M; m++) {
-            st.h0[m] = *(const u32x4*)(a.xh + r0 + k + 8 * m);
-            st.l0[m] = *(const u32x4*)(a.xl + r0 + k + 8 * m);
+            st.h0[m] = *(const u32x4*)(a.xh + frag_off(0, c, m, lane, n_c, M));
+            st.l0[m] = *(const u32x4*)(a.xl + frag_off(0, c, m, lane, n_c, M));
         }
         if (n_tt > 1) {
 #pragma unroll
             for (int m = 0; m < M; m++) {
-                st.h1[m] = *(const u32x4*)(a.xh + r1 + k + 8 * m);
-                st.l1[m] = *(const u32x4*)(a.xl + r1 + k + 8 * m);
+                st.h1[m] = *(const u32x4*)(a.xh + frag_off(1, c, m, lane, n_c, M));
+                st.l1[m] = *(const u32x4*)(a.xl + frag_off(1, c, m, lane, n_c, M));
             }
         }
     };
@@ -289,7 +318,7 @@ __global__ __launch_bounds__(PF_THREADS) void prefill_gemm16_kernel(const PfGemm
     // 4-deep ring over chunk pairs (2E k per stage); kslice % (8E) == 0 (host-checked);
     // clamped indices keep every load unconditional
     const int P = kslice / (2 * E);
-    auto ld = [&](Stage& st, const int c) { load(st, k0 + 2 * E * min(c, P - 1)); };
+    auto ld = [&](Stage& st, const int c) { load(st, k0 / (2 * E) + min(c, P - 1)); };
     Stage s0, s1, s2, s3;
     ld(s0, 0);
     ld(s1, 1);

@@ -115,7 +115,9 @@ struct xh_ctx {
     bool qaw_ok = true;            // cleared when a launch reports the shape unsupported
     // batched prefill (prefill.h), buffers allocated on first use
     bool prefill_batched = true;
-    bool prefill_f16 = false;                    // XH_OPT_PREFILL 2: split-f16 MFMA GEMMs
+    // XH_OPT_PREFILL: 1 = split-f16 GEMMs for fp8 weights (measured faster), f32 MFMA otherwise;
+    // 2 = split-f16 wherever the weights convert exactly; 3 = f32 MFMA only
+    int prefill_gemm = 1;
     bool pf_alloc = false;
     uint16_t *pf_xh = nullptr, *pf_xl = nullptr; // [PF_TOK][max K] f16 halves of a GEMM input
     float* pf_xs = nullptr;                      // [PF_TOK] 1 / row scale
@@ -736,7 +738,8 @@ int pf_gemm16(xh_ctx* ctx, int dt, const void* w, int K, int rows, const float* 
     const int E = elems_per_16b(dt);
     const int ks = pf_ks16(rows, K, E);
     if (!ks) return 0;
-    hipLaunchKernelGGL(prefill_split_kernel, dim3(n), dim3(256), 0, ctx->stream, x, K, ctx->pf_xh, ctx->pf_xl, ctx->pf_xs);
+    hipLaunchKernelGGL(prefill_split_kernel, dim3(32 * ((n + 31) / 32)), dim3(256), 0, ctx->stream, x, K, n, E,
+                       ctx->pf_xh, ctx->pf_xl, ctx->pf_xs);
     PfGemm16Args a{};
     a.w = w; a.row_bytes = (size_t)K * (16 / E); a.K = K; a.rows = rows;
     a.xh = ctx->pf_xh; a.xl = ctx->pf_xl; a.inv_s = ctx->pf_xs; a.n = n; a.ks = ks; a.part = ctx->pf_part;
@@ -749,7 +752,8 @@ int pf_gemm16(xh_ctx* ctx, int dt, const void* w, int K, int rows, const float* 
 }
 // Y partials of W[rows][K] . X[n][K]; returns ks (0: dtype / shape not supported)
 int pf_gemm(xh_ctx* ctx, int dt, const void* w, int K, int rows, const float* x, int n) {
-    if (ctx->prefill_f16) {
+    const bool f8 = dt == XH_F8_E4M3 || dt == XH_F8_E5M2;
+    if (ctx->prefill_gemm == 2 || (ctx->prefill_gemm == 1 && f8)) {
         const int ks = pf_gemm16(ctx, dt, w, K, rows, x, n);
         if (ks) return ks;
     }
@@ -1608,7 +1612,7 @@ int xh_get_option(const xh_ctx* ctx, int option, int* value) {
             *value = ctx->fuse_level >= 2 && ctx->qaw_ok && aw_instantiated(ctx->c.head_dim, ctx->qpk) ? 2
                      : ctx->fuse_attn_wo ? 1 : 0;
             return 0;
-        case XH_OPT_PREFILL: *value = !ctx->prefill_batched ? 0 : ctx->prefill_f16 ? 2 : 1; return 0;
+        case XH_OPT_PREFILL: *value = ctx->prefill_batched ? ctx->prefill_gemm : 0; return 0;
         default: return XH_E_INVALID;
     }
 }
@@ -1628,9 +1632,9 @@ int xh_set_option(xh_ctx* ctx, int option, int value) {
             drop_graphs(ctx);
             return 0;
         case XH_OPT_PREFILL:
-            if (value < 0 || value > 2) return set_err(ctx, XH_E_INVALID, "XH_OPT_PREFILL: 0, 1 or 2");
+            if (value < 0 || value > 3) return set_err(ctx, XH_E_INVALID, "XH_OPT_PREFILL: 0 ... 3");
             ctx->prefill_batched = value != 0;
-            ctx->prefill_f16 = value == 2;
+            if (value) ctx->prefill_gemm = value;
             return 0;
         default: return set_err(ctx, XH_E_INVALID, "unknown option %d", option);
     }
