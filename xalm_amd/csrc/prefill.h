@@ -219,6 +219,68 @@ __global__ __launch_bounds__(256) void prefill_split_kernel(const float* x, int 
     if (threadIdx.x == 0) inv_s[t] = 1.f / s;
 }
 
+// rmsnorm of each token row (as prefill_rmsnorm_kernel: x * scale * w, same reduction) written
+// straight into the split-f16 fragment layout for the GEMM that consumes it: one launch instead
+// of rmsnorm + split (grid = 32 x token tiles; rows past n are zero)
+__global__ __launch_bounds__(256) void prefill_rmsnorm_split_kernel(const float* x, int dim, const void* w, int wdt,
+                                                                    float eps, int n, int E, uint16_t* xh,
+                                                                    uint16_t* xl, float* inv_s) {
+    __shared__ float red[4];
+    const int t = blockIdx.x;
+    const int M = E / 8, n_c = dim / (2 * E);
+    auto frag = [&](const int k) {
+        const int c = k / (2 * E), r = k - c * 2 * E, hh = r / E, m = (r - hh * E) / 8;
+        return frag_off(t >> 5, c, m, (t & 31) + 32 * hh, n_c, M);
+    };
+    if (t >= n) {
+        for (int i = threadIdx.x; i < dim / 8; i += 256) {
+            const size_t o = frag(8 * i);
+            *(u32x4*)(xh + o) = u32x4{0u, 0u, 0u, 0u};
+            *(u32x4*)(xl + o) = u32x4{0u, 0u, 0u, 0u};
+        }
+        return;
+    }
+    const float* xr = x + (size_t)t * dim;
+    const float scale = block_rms_scale<256>(xr, dim, eps, red);
+    __syncthreads();  // red reused below
+    auto norm8 = [&](const int i, float* v) {  // elements 8i .. 8i+7 of the normed row
+        const float4 a = ((const float4*)xr)[2 * i], b = ((const float4*)xr)[2 * i + 1];
+        const float4 wa = load_norm4(w, wdt, 2 * i), wb = load_norm4(w, wdt, 2 * i + 1);
+        v[0] = a.x * scale * wa.x; v[1] = a.y * scale * wa.y; v[2] = a.z * scale * wa.z; v[3] = a.w * scale * wa.w;
+        v[4] = b.x * scale * wb.x; v[5] = b.y * scale * wb.y; v[6] = b.z * scale * wb.z; v[7] = b.w * scale * wb.w;
+    };
+    float m = 0.f;
+    for (int i = threadIdx.x; i < dim / 8; i += 256) {
+        float v[8];
+        norm8(i, v);
+#pragma unroll
+        for (int j = 0; j < 8; j++) m = fmaxf(m, fabsf(v[j]));
+    }
+    m = wave_max(m);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+    __syncthreads();
+    m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    int e = 0;
+    const bool ok = m > 0.f && m <= FLT_MAX;
+    if (ok) frexpf(m, &e);
+    const float s = ok ? ldexpf(1.f, 15 - e) : 1.f;
+    for (int i = threadIdx.x; i < dim / 8; i += 256) {
+        float v[8];
+        norm8(i, v);
+        f16x8 hi, lo;
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const float u = v[j] * s;
+            hi[j] = (_Float16)u;
+            lo[j] = (_Float16)(u - (float)hi[j]);
+        }
+        const size_t o = frag(8 * i);
+        *(f16x8*)(xh + o) = hi;
+        *(f16x8*)(xl + o) = lo;
+    }
+    if (threadIdx.x == 0) inv_s[t] = 1.f / s;
+}
+
 // 16 weight bytes -> E/8 B operands of 8 f16 (k order = byte order)
 template <int DT>
 __device__ __forceinline__ void w_f16(const u32x4 w, f16x8* b) {

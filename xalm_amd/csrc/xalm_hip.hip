@@ -118,6 +118,7 @@ struct xh_ctx {
     // XH_OPT_PREFILL: 1 = split-f16 GEMMs for fp8 weights (measured faster), f32 MFMA otherwise;
     // 2 = split-f16 wherever the weights convert exactly; 3 = f32 MFMA only
     int prefill_gemm = 1;
+    bool pf_split_ready = false;                 // pf_norm left the next GEMM's split input
     bool pf_alloc = false;
     uint16_t *pf_xh = nullptr, *pf_xl = nullptr; // [PF_TOK][max K] f16 halves of a GEMM input
     float* pf_xs = nullptr;                      // [PF_TOK] 1 / row scale
@@ -732,14 +733,39 @@ void pf_gemm16_t(const PfGemm16Args& a, hipStream_t s) {
     hipLaunchKernelGGL((prefill_gemm16_kernel<DT, PF_RT16>), dim3((waves + PF_WAVES - 1) / PF_WAVES), dim3(PF_THREADS),
                        0, s, a);
 }
-// the split-f16 form of pf_gemm (XH_OPT_PREFILL 2) for weights exact in f16; 0 = not taken
-int pf_gemm16(xh_ctx* ctx, int dt, const void* w, int K, int rows, const float* x, int n) {
-    if (dt != XH_F16 && dt != XH_F8_E4M3 && dt != XH_F8_E5M2) return 0;
+// E of the split-f16 path when the GEMM over W (dtype dt, [rows][K]) takes it, else 0
+// (XH_OPT_PREFILL 1: fp8 weights; 2: f16 and fp8; 3: never; a K slicing must exist)
+int pf_split_E(const xh_ctx* ctx, int dt, int K, int rows) {
+    const bool f8 = dt == XH_F8_E4M3 || dt == XH_F8_E5M2;
+    if (!(ctx->prefill_gemm == 2 || (ctx->prefill_gemm == 1 && f8))) return 0;
+    if (dt != XH_F16 && !f8) return 0;
     const int E = elems_per_16b(dt);
+    return pf_ks16(rows, K, E) ? E : 0;
+}
+// rmsnorm of the pass's rows (pf_x) as the input of the GEMM over W (dt, [rows][dim]): written
+// straight into the split-f16 fragments when that GEMM takes the split path (one launch)
+void pf_norm(xh_ctx* ctx, const void* nw, int ndt, int m, int dt, int rows) {
+    const xh_config& c = ctx->c;
+    const int E = pf_split_E(ctx, dt, c.dim, rows);
+    if (E) {
+        hipLaunchKernelGGL(prefill_rmsnorm_split_kernel, dim3(32 * ((m + 31) / 32)), dim3(256), 0, ctx->stream,
+                           (const float*)ctx->pf_x, c.dim, nw, ndt, c.norm_eps, m, E, ctx->pf_xh, ctx->pf_xl, ctx->pf_xs);
+        ctx->pf_split_ready = true;
+    } else {
+        hipLaunchKernelGGL(prefill_rmsnorm_kernel, dim3(m), dim3(256), 0, ctx->stream, (const float*)ctx->pf_x, c.dim,
+                           nw, ndt, c.norm_eps, ctx->pf_xn);
+    }
+}
+// the split-f16 form of pf_gemm for weights exact in f16; 0 = not taken
+int pf_gemm16(xh_ctx* ctx, int dt, const void* w, int K, int rows, const float* x, int n) {
+    const int E = pf_split_E(ctx, dt, K, rows);
+    if (!E) return 0;
     const int ks = pf_ks16(rows, K, E);
-    if (!ks) return 0;
-    hipLaunchKernelGGL(prefill_split_kernel, dim3(32 * ((n + 31) / 32)), dim3(256), 0, ctx->stream, x, K, n, E,
-                       ctx->pf_xh, ctx->pf_xl, ctx->pf_xs);
+    if (ctx->pf_split_ready)
+        ctx->pf_split_ready = false;  // pf_norm wrote the fragments of x
+    else
+        hipLaunchKernelGGL(prefill_split_kernel, dim3(32 * ((n + 31) / 32)), dim3(256), 0, ctx->stream, x, K, n, E,
+                           ctx->pf_xh, ctx->pf_xl, ctx->pf_xs);
     PfGemm16Args a{};
     a.w = w; a.row_bytes = (size_t)K * (16 / E); a.K = K; a.rows = rows;
     a.xh = ctx->pf_xh; a.xl = ctx->pf_xl; a.inv_s = ctx->pf_xs; a.n = n; a.ks = ks; a.part = ctx->pf_part;
@@ -752,8 +778,7 @@ int pf_gemm16(xh_ctx* ctx, int dt, const void* w, int K, int rows, const float* 
 }
 // Y partials of W[rows][K] . X[n][K]; returns ks (0: dtype / shape not supported)
 int pf_gemm(xh_ctx* ctx, int dt, const void* w, int K, int rows, const float* x, int n) {
-    const bool f8 = dt == XH_F8_E4M3 || dt == XH_F8_E5M2;
-    if (ctx->prefill_gemm == 2 || (ctx->prefill_gemm == 1 && f8)) {
+    {
         const int ks = pf_gemm16(ctx, dt, w, K, rows, x, n);
         if (ks) return ks;
     }
@@ -827,6 +852,7 @@ int prefill_batched(xh_ctx* ctx, const int* tokens, int n, int pos0, int want_lo
     const xh_config& c = ctx->c;
     int rc = pf_alloc(ctx);
     if (rc) return rc;
+    ctx->pf_split_ready = false;
     if (probs && !ctx->pf_logits &&
         ((rc = dmalloc(ctx, &ctx->pf_logits, (size_t)PF_TOK * c.vocab_size)) || (rc = dmalloc(ctx, &ctx->pf_tgt, (size_t)PF_TOK))))
         return rc;
@@ -852,9 +878,8 @@ int prefill_batched(xh_ctx* ctx, const int* tokens, int n, int pos0, int want_lo
         for (int l = 0; l < c.n_layers; l++) {
             const LayerW& w = ctx->L[l];
             // attention block (src/infer.cpp:380-452)
-            hipLaunchKernelGGL(prefill_rmsnorm_kernel, dim3(m), dim3(256), 0, ctx->stream, (const float*)ctx->pf_x, c.dim,
-                               (const void*)w.attn_norm, w.an_dt, c.norm_eps, ctx->pf_xn);
             const int qkv_rows = ctx->q_dim + 2 * ctx->kv_dim;
+            pf_norm(ctx, w.attn_norm, w.an_dt, m, kdt(w.qkv_dt, w.qkv_x), qkv_rows);
             int ks = pf_gemm(ctx, kdt(w.qkv_dt, w.qkv_x), w.wqkv, c.dim, qkv_rows, ctx->pf_xn, m);
             if (!ks) return set_err(ctx, XH_E_INVALID, "prefill: qkv shape not supported");
             PfEpiArgs e{};
@@ -874,8 +899,7 @@ int prefill_batched(xh_ctx* ctx, const int* tokens, int n, int pos0, int want_lo
             e.ks = ks; e.n = m; e.rows = c.dim; e.epi = EPI_RESID; e.out = ctx->pf_x;
             pf_epi(ctx, e);
             // feed-forward block (src/infer.cpp:455-494)
-            hipLaunchKernelGGL(prefill_rmsnorm_kernel, dim3(m), dim3(256), 0, ctx->stream, (const float*)ctx->pf_x, c.dim,
-                               (const void*)w.ffn_norm, w.fn_dt, c.norm_eps, ctx->pf_xn);
+            pf_norm(ctx, w.ffn_norm, w.fn_dt, m, kdt(w.w13_dt, w.w13_x), 2 * c.hidden_dim);
             ks = pf_gemm(ctx, kdt(w.w13_dt, w.w13_x), w.w13, c.dim, 2 * c.hidden_dim, ctx->pf_xn, m);
             if (!ks) return set_err(ctx, XH_E_INVALID, "prefill: w1/w3 shape not supported");
             e = PfEpiArgs{};
