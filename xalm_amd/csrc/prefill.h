@@ -4,7 +4,9 @@
 // per token.  Same math per token as the decode path (src/infer.cpp:365-496); the matrix
 // products run on the f32-input MFMA (v_mfma_f32_32x32x2_f32: exact f32 products, f32
 // accumulation — a k-ordered fmaf chain, MI355X_MICROARCH.md "Matrix cores"), so activations
-// stay f32 exactly as in the reference; only the summation order differs.
+// stay f32 exactly as in the reference and only the summation order differs — or, for fp8
+// weights by default (XH_OPT_PREFILL), on the split-f16 MFMA below (activations as exact
+// f16 hi + lo pairs, ≈22-bit mantissa).
 //
 // GEMM layout: Y[t][r] = sum_k X[t][k] W[r][k], W row-major [rows][K] as uploaded.  One wave
 // owns RT 32-row tiles x one K slice x up to 64 tokens (2 RT 32x32 f32 accumulators).  Lane l
