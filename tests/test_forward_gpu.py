@@ -371,6 +371,19 @@ def test_perplexity_token_loop_paths(case):
     check_probs(gm.token_probs(toks), om, toks)
 
 
+def test_prefill_option_values():
+    xf = XalmFile(fixture_path("tiny_mistral_f16.xalm"))
+    gm = Model.from_xalm(xf)
+    assert gm.get_option(L.OPT_PREFILL) == 1
+    for v in (0, 2, 3, 1):
+        gm.set_option(L.OPT_PREFILL, v)
+        assert gm.get_option(L.OPT_PREFILL) == v
+    for bad in (-1, 4):
+        with pytest.raises(L.XhError):
+            gm.set_option(L.OPT_PREFILL, bad)
+    assert gm.get_option(L.OPT_PREFILL) == 1
+
+
 def test_perplexity_arguments():
     xf = XalmFile(fixture_path("tiny_mistral_f16.xalm"))
     gm = Model.from_xalm(xf)
