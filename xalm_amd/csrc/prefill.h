@@ -283,6 +283,66 @@ __global__ __launch_bounds__(256) void prefill_rmsnorm_split_kernel(const float*
     if (threadIdx.x == 0) inv_s[t] = 1.f / s;
 }
 
+// EPI_GLU (act(g) * u of the summed K-slices, slice order as prefill_epi_kernel) written
+// straight into the split-f16 fragments of the W2 GEMM's input: one launch instead of GLU
+// epilogue + split.  The row (hidden f32) is held in dynamic LDS between the max and the split
+// (grid = 32 x token tiles; rows past n are zero)
+__global__ __launch_bounds__(1024) void prefill_glu_split_kernel(const float* part, int ks, int n, int hidden, int act,
+                                                                int E, uint16_t* xh, uint16_t* xl, float* inv_s) {
+    extern __shared__ float hrow[];
+    __shared__ float red[16];
+    const int t = blockIdx.x;
+    const int M = E / 8, n_c = hidden / (2 * E);
+    auto frag = [&](const int k) {
+        const int c = k / (2 * E), r = k - c * 2 * E, hh = r / E, m = (r - hh * E) / 8;
+        return frag_off(t >> 5, c, m, (t & 31) + 32 * hh, n_c, M);
+    };
+    if (t >= n) {
+        for (int i = threadIdx.x; i < hidden / 8; i += 1024) {
+            const size_t o = frag(8 * i);
+            *(u32x4*)(xh + o) = u32x4{0u, 0u, 0u, 0u};
+            *(u32x4*)(xl + o) = u32x4{0u, 0u, 0u, 0u};
+        }
+        return;
+    }
+    const size_t rows = 2 * (size_t)hidden;
+    float m = 0.f;
+#pragma unroll 4
+    for (int i = threadIdx.x; i < hidden; i += 1024) {
+        float v0 = 0.f, v1 = 0.f;
+        for (int s = 0; s < ks; s++) {  // slice order: fixed
+            const float2 p = *(const float2*)(part + ((size_t)s * n + t) * rows + 2 * i);
+            v0 += p.x;
+            v1 += p.y;
+        }
+        const float h = act_fn(act, v0) * v1;
+        hrow[i] = h;
+        m = fmaxf(m, fabsf(h));
+    }
+    m = wave_max(m);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+    __syncthreads();
+    m = red[0];
+    for (int w = 1; w < 16; w++) m = fmaxf(m, red[w]);
+    int e = 0;
+    const bool ok = m > 0.f && m <= FLT_MAX;
+    if (ok) frexpf(m, &e);
+    const float s = ok ? ldexpf(1.f, 15 - e) : 1.f;
+    for (int i = threadIdx.x; i < hidden / 8; i += 1024) {
+        f16x8 hi, lo;
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const float u = hrow[8 * i + j] * s;
+            hi[j] = (_Float16)u;
+            lo[j] = (_Float16)(u - (float)hi[j]);
+        }
+        const size_t o = frag(8 * i);
+        *(f16x8*)(xh + o) = hi;
+        *(f16x8*)(xl + o) = lo;
+    }
+    if (threadIdx.x == 0) inv_s[t] = 1.f / s;
+}
+
 // 16 weight bytes -> E/8 B operands of 8 f16 (k order = byte order)
 template <int DT>
 __device__ __forceinline__ void w_f16(const u32x4 w, f16x8* b) {

@@ -902,9 +902,18 @@ int prefill_batched(xh_ctx* ctx, const int* tokens, int n, int pos0, int want_lo
             pf_norm(ctx, w.ffn_norm, w.fn_dt, m, kdt(w.w13_dt, w.w13_x), 2 * c.hidden_dim);
             ks = pf_gemm(ctx, kdt(w.w13_dt, w.w13_x), w.w13, c.dim, 2 * c.hidden_dim, ctx->pf_xn, m);
             if (!ks) return set_err(ctx, XH_E_INVALID, "prefill: w1/w3 shape not supported");
-            e = PfEpiArgs{};
-            e.ks = ks; e.n = m; e.rows = 2 * c.hidden_dim; e.epi = EPI_GLU; e.out = ctx->pf_h; e.act = c.act;
-            pf_epi(ctx, e);
+            const int E2 = pf_split_E(ctx, kdt(w.w2_dt, w.w2_x), c.hidden_dim, c.dim);
+            if (E2 && (size_t)c.hidden_dim * sizeof(float) <= 64 * 1024) {
+                // GLU epilogue straight into the W2 GEMM's split-f16 fragments (one launch)
+                hipLaunchKernelGGL(prefill_glu_split_kernel, dim3(32 * ((m + 31) / 32)), dim3(1024),
+                                   (size_t)c.hidden_dim * sizeof(float), ctx->stream, (const float*)ctx->pf_part, ks,
+                                   m, c.hidden_dim, c.act, E2, ctx->pf_xh, ctx->pf_xl, ctx->pf_xs);
+                ctx->pf_split_ready = true;
+            } else {
+                e = PfEpiArgs{};
+                e.ks = ks; e.n = m; e.rows = 2 * c.hidden_dim; e.epi = EPI_GLU; e.out = ctx->pf_h; e.act = c.act;
+                pf_epi(ctx, e);
+            }
             ks = pf_gemm(ctx, kdt(w.w2_dt, w.w2_x), w.w2, c.hidden_dim, c.dim, ctx->pf_h, m);
             if (!ks) return set_err(ctx, XH_E_INVALID, "prefill: w2 shape not supported");
             e = PfEpiArgs{};
