@@ -37,7 +37,12 @@ $(OBJ)/xalm_hip.o: $(HIP_SRC) $(HIP_HDR)
 $(OBJ)/dt_launch_dt%.o: xalm_amd/csrc/dt_launch.hip $(HIP_HDR)
 	@mkdir -p $(OBJ)
 	$(HIPCC) $(HIPFLAGS) -DPK_DT=$* -c -o $@ $<
-$(LIB)/libxalm_hip.so: $(OBJ)/xalm_hip.o $(PK_OBJS)
+SE_DTS := 1 2 3 6 7
+SE_OBJS := $(patsubst %,$(OBJ)/se_launch_dt%.o,$(SE_DTS))
+$(OBJ)/se_launch_dt%.o: xalm_amd/csrc/se_launch.hip $(HIP_HDR)
+	@mkdir -p $(OBJ)
+	$(HIPCC) $(HIPFLAGS) -DSE_DT=$* -c -o $@ $<
+$(LIB)/libxalm_hip.so: $(OBJ)/xalm_hip.o $(PK_OBJS) $(SE_OBJS)
 	@mkdir -p $(LIB)
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $^
 

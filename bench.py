@@ -179,8 +179,8 @@ def main():
     ap.add_argument("--cpu-tokens", type=int, default=4)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--kernel-iters", type=int, default=200)
-    ap.add_argument("--engine", type=int, default=-1, choices=(-1, 0, 1),
-                    help="-1 auto (persistent kernel when instantiated), 0 graph of kernels, 1 persistent")
+    ap.add_argument("--engine", type=int, default=-1, choices=(-1, 0, 1, 2),
+                    help="-1 auto, 0 graph of kernels, 1 persistent kernel, 2 stream kernel (LDS-DMA weight ring)")
     ap.add_argument("--prefill-mode", type=int, default=1, choices=(1, 2, 3),
                     help="batched prefill GEMMs (XH_OPT_PREFILL): 1 default per dtype, 2 split-f16 MFMA "
                          "wherever the weights allow, 3 f32-input MFMA only")
@@ -231,7 +231,7 @@ def main():
         raise SystemExit(f"steps exceed the {c.max_seq_len} context")
 
     toks, elapsed = timed_region(dist, torch_mod, lambda: model.decode_greedy(pos, args.steps))
-    launch_us = model.last_launch_us() if engine == 1 else None
+    launch_us = model.last_launch_us() if engine in (1, 2) else None
     assert len(toks) == args.steps
 
     # algorithmic bytes of the timed tokens: Model::active_bytes(pos) (src/model.cpp:12-35)
@@ -287,12 +287,13 @@ def main():
         if n:
             cpu = cpu_baseline(w, c, prompt, logits0, warm_tokens, n)
 
-    if engine == 1:
-        # dominant (only) kernel: the persistent decode kernel; one launch = the K timed tokens
+    if engine in (1, 2):
+        # dominant (only) kernel: the one-launch decode kernel; one launch = the K timed tokens
         r_gbps = step_bytes / (launch_us * 1e-6) / 1e9
+        kname = "persistent_decode_kernel" if engine == 1 else "stream_decode_kernel"
         roofline = {"bound": "hbm", "achieved": round(r_gbps, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                     "frac": round(r_gbps / HBM_PEAK_GBPS, 4), "traffic": None,
-                    "kernel": "persistent_decode_kernel (all phases of all timed tokens, one launch)",
+                    "kernel": kname + " (all phases of all timed tokens, one launch)",
                     "bytes_per_launch": step_bytes, "avg_launch_us": round(launch_us, 1)}
     else:
         # the W1/W3 launch's exact instantiation (PF shape, see xalm_hip.hip launch_gemv_t)
@@ -320,7 +321,7 @@ def main():
             "data": "synthetic (deterministic xalm_synth weights of the named shapes; no checkpoint offline)",
             "config": {"workload": w["desc"], "prompt_tokens": len(prompt), "max_seq_len": c.max_seq_len,
                        "kv_len_timed": [pos + 1, pos + args.steps], "batch": 1, "parallelism": f"replicas x{world}",
-                       "engine": "persistent" if engine == 1 else
+                       "engine": "persistent" if engine == 1 else "stream (LDS-DMA weight ring)" if engine == 2 else
                        {2: "graph, qkv+attention+Wo fused", 1: "graph, attention+Wo fused",
                         0: "graph"}[model.get_option(L.OPT_FUSE_ATTN_WO)]},
             "roofline": roofline,

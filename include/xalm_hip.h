@@ -147,9 +147,13 @@ int xh_perplexity(xh_ctx* ctx, const int* tokens, int n, int pos0, float* probs_
 
 /* Device engine: 0 = one hipGraph of kernels per token (gemv / attention launches);
  * 1 = the persistent decode kernel (one launch per call, every phase inside, weights
- * streamed ahead across the hand-offs; needs one dtype for all layer matrices and norms and
- * an instantiated head shape); -1 = automatic (currently the graph engine, the faster one on
- * MI355X).  Both compute the same math (reduction orders differ, within the tolerances). */
+ * prefetched into registers across the hand-offs); 2 = the stream kernel (one launch per
+ * call; one loader wave per CU streams every weight row through an LDS-DMA ring ahead of the
+ * hand-offs, consumer waves compute from the ring).  1 and 2 need one dtype for all layer
+ * matrices and norms and an instantiated head shape; 2 also rows of whole 1 KiB (f16: dim,
+ * q_dim and hidden multiples of 512).  -1 = automatic (currently the graph engine).  All
+ * compute the same math (reduction orders differ, within the tolerances); xh_set_engine
+ * returns XH_E_INVALID for an engine that cannot run these weights. */
 int xh_set_engine(xh_ctx* ctx, int engine);
 int xh_get_engine(const xh_ctx* ctx); /* the engine the next call will use */
 /* Device time (HIP events on the context's stream) of the last persistent-engine launch,
@@ -161,7 +165,11 @@ int xh_last_launch_us(const xh_ctx* ctx, float* us);
  * overwrites), 0 = off, -1 = unchanged.  Copies min(cap, *len) words of the last traced launch
  * to `out` first.  Persistent engine: for the launch's last token, workgroups {0, n_cu/2, n_cu-1} x [n_layers + 1][5 phases][2] device
  * clock stamps (100 MHz; 0 = not reached) — [l][p][0] hand-off passed, [l][p][1] published —
- * plus 2 words ([n_layers][1][1] = token start, [n_layers][1][0] = next token known). */
+ * plus 2 words ([n_layers][1][1] = token start, [n_layers][1][0] = next token known).
+ * 8 = stream engine: [n_cu][4] device-clock sums (loader waiting for a free ring slot,
+ * consumer wave 0 waiting for a full slot, its hand-off waits, its attention), then for the
+ * last token of CUs {0, n_cu/2, n_cu-1} [4 n_layers + 1 phases][4] stamps: input wait start,
+ * input ready, matrix done, first slot issued by the loader. */
 int xh_debug_trace(xh_ctx* ctx, int enable, uint64_t* out, int cap, int* len);
 
 /* Copy the current device logits to the host. */

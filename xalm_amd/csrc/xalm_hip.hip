@@ -40,6 +40,7 @@
 #include "gemv.h"
 #include "dt_launch.h"
 #include "prefill.h"
+#include "se_launch.h"
 #include "standalone.h"
 
 using namespace xalm;
@@ -141,7 +142,7 @@ struct xh_ctx {
     hipGraphExec_t g_logits = nullptr, g_hydrate = nullptr, g_decode = nullptr;
     int max_gemv_waves = 4096;  // 16 waves per CU
     // persistent engine (persistent.h)
-    int engine = -1;            // -1 auto, 0 graph of kernels, 1 persistent
+    int engine = -1;            // -1 auto, 0 graph of kernels, 1 persistent, 2 stream (stream.h)
     int n_cu = 0;
     PkLayer* pk_layers = nullptr;        // device [n_layers]
     unsigned* pk_counters = nullptr;     // device [n_layers * PK_PHASES + 1][PK_CSLOT] (sharded)
@@ -158,6 +159,17 @@ struct xh_ctx {
     bool pk_trace_on = false;
     bool aw_trace_on = false;  // fused attention + Wo launches write pk_trace (debug)
     bool qaw_trace_on = false;  // fused qkv + attention + Wo launches write pk_trace (debug)
+    bool se_trace_on = false;   // stream kernel writes pk_trace (debug, stream.h SeArgs::trace)
+    // stream engine (stream.h): hand-off buffers, zeroed before every launch
+    SeLayer* se_layers = nullptr;            // device [n_layers]
+    unsigned long long* se_g = nullptr;      // device granules: x [dim], hb [hidden], attn [q_dim], cand [n_cu]
+    size_t se_g_words = 0;
+    unsigned* se_qcnt = nullptr;             // device [n_layers][n_kv_heads]
+    int* se_tickets = nullptr;               // device [n_kv_heads]
+    float *se_part_o = nullptr, *se_part_ml = nullptr;  // device [se_max_splits][n_heads][head_dim | 2]
+    int se_max_splits = 1;
+    int se_nslots = 0;                       // ring slots per CU (0: engine unavailable)
+    bool se_layers_dirty = true;
 
     uint16_t* kcache(int l) { return kv + (size_t)l * 2 * c.max_seq_len * kv_dim; }
     uint16_t* vcache(int l) { return kcache(l) + (size_t)c.max_seq_len * kv_dim; }
@@ -518,14 +530,13 @@ int pk_nsplit(const xh_ctx* ctx) {
     return ns < 1 ? 1 : ns;
 }
 
-// the weight dtypes the persistent kernel is instantiated for, or false
-bool pk_dtypes(const xh_ctx* ctx, int* dt, int* dtc, int* norm_dt) {
+// One dtype for every matrix and one for every norm (the one-launch engines' kernels are
+// instantiated per matrix dtype), no fp8 matrix that needs the exact bit decode, and an
+// lm_head dtype the instantiations cover (fp8 models: bf16 per convert.py, or fp8).
+bool uniform_dtypes(const xh_ctx* ctx, int* dt, int* dtc, int* norm_dt) {
     if (ctx->wcls_x) return false;
     for (const LayerW& w : ctx->L)
         if (w.qkv_x || w.w13_x || w.wo_x || w.w2_x) return false;  // exact fp8 decode: graph engine
-    // pk_stage holds at most 8 float4 of x per thread
-    if (ctx->c.hidden_dim > 32 * PK_THREADS || ctx->c.dim > 32 * PK_THREADS || ctx->q_dim > 32 * PK_THREADS) return false;
-    const xh_config& c = ctx->c;
     *dt = ctx->L[0].qkv_dt;
     *norm_dt = ctx->L[0].an_dt;
     for (const LayerW& w : ctx->L)
@@ -534,9 +545,6 @@ bool pk_dtypes(const xh_ctx* ctx, int* dt, int* dtc, int* norm_dt) {
             return false;
     if (ctx->final_norm_dt != *norm_dt) return false;
     *dtc = ctx->wcls_dt;
-    const bool hd_ok = (c.head_dim == 128 && (ctx->qpk == 4 || ctx->qpk == 8)) || (c.head_dim == 16 && ctx->qpk == 2) ||
-                       (c.head_dim == 64 && ctx->qpk == 4);
-    if (!hd_ok) return false;
     switch (*dt) {
         case XH_F16: return *dtc == XH_F16;
         case XH_BF16: return *dtc == XH_BF16;
@@ -547,17 +555,33 @@ bool pk_dtypes(const xh_ctx* ctx, int* dt, int* dtc, int* norm_dt) {
     }
 }
 
+// the weight dtypes the persistent kernel is instantiated for, or false
+bool pk_dtypes(const xh_ctx* ctx, int* dt, int* dtc, int* norm_dt) {
+    if (!uniform_dtypes(ctx, dt, dtc, norm_dt)) return false;
+    // pk_stage holds at most 8 float4 of x per thread
+    if (ctx->c.hidden_dim > 32 * PK_THREADS || ctx->c.dim > 32 * PK_THREADS || ctx->q_dim > 32 * PK_THREADS) return false;
+    const xh_config& c = ctx->c;
+    return (c.head_dim == 128 && (ctx->qpk == 4 || ctx->qpk == 8)) || (c.head_dim == 16 && ctx->qpk == 2) ||
+           (c.head_dim == 64 && ctx->qpk == 4);
+}
+
 // automatic selection = the graph engine: measured faster on MI355X (3.0 vs 4.3 ms per
 // Mistral-7B token; the persistent kernel's one-counter hand-offs cost ~45 us per layer)
+bool se_supported(const xh_ctx* ctx, int* dt, int* dtc, int* norm_dt);
+// a one-launch engine (1: persistent.h, 2: stream.h) is selected and handles these weights
 bool use_persistent(xh_ctx* ctx) {
     int dt, dtc, ndt;
+    if (ctx->engine == 2) return se_supported(ctx, &dt, &dtc, &ndt);
     if (ctx->engine != 1) return false;
     return pk_dtypes(ctx, &dt, &dtc, &ndt);
 }
+int run_stream(xh_ctx* ctx, const int* prompt, int n_prompt, int n_gen, int pos0, int logits_last, int stop_a,
+               int stop_b, int* n_done_out);
 
 // One persistent launch: n_prompt tokens from `prompt` (host), then n_gen greedy tokens.
 int run_persistent(xh_ctx* ctx, const int* prompt, int n_prompt, int n_gen, int pos0, int logits_last, int stop_a,
                    int stop_b, int* n_done_out) {
+    if (ctx->engine == 2) return run_stream(ctx, prompt, n_prompt, n_gen, pos0, logits_last, stop_a, stop_b, n_done_out);
     ctx->cand_valid = false;  // its logits come without lm_head candidates
     const xh_config& c = ctx->c;
     int dt, dtc, ndt;
@@ -616,8 +640,115 @@ int run_persistent(xh_ctx* ctx, const int* prompt, int n_prompt, int n_gen, int 
     return 0;
 }
 
+// ---------------------------------------------------------------------------------------
+// stream engine (stream.h)
+// ---------------------------------------------------------------------------------------
+// The weights and shapes the stream kernel handles: one dtype for every matrix and one for
+// every norm (as the persistent engine), rows of whole 1 KiB K-steps, each consumer wave's
+// activations within SE_XF registers, an instantiated head shape.  Else false (graph engine).
+bool se_supported(const xh_ctx* ctx, int* dt, int* dtc, int* norm_dt) {
+    int d, dc, nd;
+    if (!uniform_dtypes(ctx, &d, &dc, &nd)) return false;
+    const xh_config& c = ctx->c;
+    if (!se_instantiated(c.head_dim, ctx->qpk) || ctx->se_nslots < SE_DEPTH + 1) return false;
+    const int E = elems_per_16b(d), EC = elems_per_16b(dc);
+    auto fits = [](int n, int e) {  // whole K-steps, at most SE_XF / e of them per consumer wave
+        if (n % (64 * e)) return false;
+        const int nk = n / (64 * e);
+        return (nk + SE_NW - 1) / SE_NW <= SE_XF / e;
+    };
+    if (!fits(c.dim, E) || !fits(ctx->q_dim, E) || !fits(c.hidden_dim, E) || !fits(c.dim, EC)) return false;
+    if (2 * ((c.dim / 2 + ctx->n_cu - 1) / ctx->n_cu) > SE_OWN_MAX) return false;  // residual rows per CU
+    if (c.vocab_size > 0x1FFFF || c.n_kv_heads > ctx->n_cu) return false;
+    *dt = d;
+    *dtc = dc;
+    *norm_dt = nd;
+    return true;
+}
+
+// One stream launch: n_prompt tokens from `prompt` (host), then n_gen greedy tokens.
+int run_stream(xh_ctx* ctx, const int* prompt, int n_prompt, int n_gen, int pos0, int logits_last, int stop_a,
+               int stop_b, int* n_done_out) {
+    ctx->cand_valid = false;  // its logits come without lm_head candidates
+    const xh_config& c = ctx->c;
+    int dt, dtc, ndt;
+    if (!se_supported(ctx, &dt, &dtc, &ndt)) return set_err(ctx, XH_E_INVALID, "stream engine not available for these weights");
+    if (n_prompt > ctx->pk_prompt_cap || n_gen > ctx->dec_cap) return set_err(ctx, XH_E_INVALID, "too many tokens");
+    if (ctx->se_layers_dirty) {
+        std::vector<SeLayer> h(c.n_layers);
+        for (int l = 0; l < c.n_layers; l++) {
+            const LayerW& w = ctx->L[l];
+            h[l] = SeLayer{w.wqkv, w.wo, w.w13, w.w2, w.attn_norm, w.ffn_norm, ctx->kcache(l), ctx->vcache(l)};
+        }
+        HIP_TRY(ctx, hipMemcpy(ctx->se_layers, h.data(), h.size() * sizeof(SeLayer), hipMemcpyHostToDevice));
+        ctx->se_layers_dirty = false;
+    }
+    if (n_prompt) {
+        memcpy(ctx->pk_host + 2, prompt, (size_t)n_prompt * sizeof(int));
+        HIP_TRY(ctx, hipMemcpyAsync(ctx->pk_prompt, ctx->pk_host + 2, (size_t)n_prompt * sizeof(int),
+                                    hipMemcpyHostToDevice, ctx->stream));
+    }
+    // every granule tag, counter and ticket starts at 0 (MI355X_MICROARCH.md: re-initialise every call)
+    HIP_TRY(ctx, hipMemsetAsync(ctx->se_g, 0, ctx->se_g_words * sizeof(unsigned long long), ctx->stream));
+    HIP_TRY(ctx, hipMemsetAsync(ctx->se_qcnt, 0, (size_t)c.n_layers * c.n_kv_heads * sizeof(unsigned), ctx->stream));
+    HIP_TRY(ctx, hipMemsetAsync(ctx->se_tickets, 0, (size_t)c.n_kv_heads * sizeof(int), ctx->stream));
+    HIP_TRY(ctx, hipMemsetAsync(ctx->pk_err, 0, 8 * sizeof(int), ctx->stream));
+    SeArgs a{};
+    a.n_layers = c.n_layers; a.dim = c.dim; a.hidden = c.hidden_dim; a.q_dim = ctx->q_dim; a.kv_dim = ctx->kv_dim;
+    a.head_dim = c.head_dim; a.n_heads = c.n_heads; a.n_kv_heads = c.n_kv_heads; a.vocab = c.vocab_size;
+    a.max_seq_len = c.max_seq_len; a.eps = c.norm_eps; a.qkv_clip = c.qkv_clip; a.act = c.act; a.norm_dt = ndt;
+    a.embed = ctx->embed; a.embed_dt = ctx->embed_dt; a.final_norm = ctx->final_norm; a.wcls = ctx->wcls;
+    a.layers = ctx->se_layers; a.rope_freq = ctx->rope_freq; a.sink_cos = ctx->sink_cos; a.sink_sin = ctx->sink_sin;
+    a.xg = ctx->se_g;
+    a.hg = a.xg + c.dim;
+    a.ag = a.hg + c.hidden_dim;
+    a.cg = a.ag + ctx->q_dim;
+    a.q = ctx->q; a.qcnt = ctx->se_qcnt; a.part_o = ctx->se_part_o; a.part_ml = ctx->se_part_ml;
+    a.tickets = ctx->se_tickets; a.logits = ctx->logits;
+    a.nslots = ctx->se_nslots;
+    // one batch of K/V row groups per attention wave (stream.h se_attention: SE_NA waves x
+    // 64 / (head_dim / 8) rows x 4)
+    a.split_rows = SE_NA * (64 / (c.head_dim / 8)) * 4;
+    a.max_splits = ctx->se_max_splits;
+    {
+        const char* ev = getenv("XALM_SE_ROTATE");  // experiment switch (default on)
+        a.rotate = ev ? atoi(ev) : 1;
+    }
+    a.err = ctx->pk_err;
+    a.prompt = ctx->pk_prompt; a.n_prompt = n_prompt; a.n_gen = n_gen; a.pos0 = pos0; a.logits_last = logits_last;
+    a.stop_a = stop_a; a.stop_b = stop_b; a.tokens_out = ctx->dec_tokens; a.n_done = ctx->pk_err + 1;
+    a.trace = ctx->se_trace_on ? ctx->pk_trace : nullptr;
+    char msg[256] = {0};
+    HIP_TRY(ctx, hipEventRecord(ctx->pk_ev[0], ctx->stream));
+    int rc;
+    switch (dt) {
+        case XH_F32: rc = se_launch_dt1(a, dtc, ctx->n_cu, ctx->stream, msg, sizeof msg); break;
+        case XH_F16: rc = se_launch_dt2(a, dtc, ctx->n_cu, ctx->stream, msg, sizeof msg); break;
+        case XH_BF16: rc = se_launch_dt3(a, dtc, ctx->n_cu, ctx->stream, msg, sizeof msg); break;
+        case XH_F8_E4M3: rc = se_launch_dt6(a, dtc, ctx->n_cu, ctx->stream, msg, sizeof msg); break;
+        case XH_F8_E5M2: rc = se_launch_dt7(a, dtc, ctx->n_cu, ctx->stream, msg, sizeof msg); break;
+        default: rc = XH_E_INVALID; snprintf(msg, sizeof msg, "stream engine: dtype %d", dt);
+    }
+    if (rc) return set_err(ctx, rc, "%s", msg);
+    HIP_TRY(ctx, hipEventRecord(ctx->pk_ev[1], ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->pk_host, ctx->pk_err, 2 * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    float ms = 0.f;
+    HIP_TRY(ctx, hipEventElapsedTime(&ms, ctx->pk_ev[0], ctx->pk_ev[1]));
+    ctx->pk_last_us = ms * 1000.f;
+    if (ctx->pk_host[0]) {
+        int info[4] = {0, 0, 0, 0};
+        hipMemcpy(info, ctx->pk_err + 2, sizeof info, hipMemcpyDeviceToHost);
+        return set_err(ctx, XH_E_HIP, "stream kernel: a wait timed out (2 s): code %d workgroup %d wave %d value %d",
+                       info[0], info[1], info[2], info[3]);
+    }
+    if (n_done_out) *n_done_out = ctx->pk_host[1];
+    return 0;
+}
+
 void drop_graphs(xh_ctx* ctx) {
     ctx->pk_layers_dirty = true;
+    ctx->se_layers_dirty = true;
     if (ctx->g_logits) hipGraphExecDestroy(ctx->g_logits);
     if (ctx->g_hydrate) hipGraphExecDestroy(ctx->g_hydrate);
     if (ctx->g_decode) hipGraphExecDestroy(ctx->g_decode);
@@ -1055,11 +1186,25 @@ int xh_create(const xh_config* cfg, int device_ordinal, xh_ctx** out) {
     CREATE_TRY(dmalloc(ctx, &ctx->pk_layers, (size_t)c.n_layers));
     CREATE_TRY(dmalloc(ctx, &ctx->pk_counters, ((size_t)c.n_layers * PK_PHASES + 1) * PK_CSLOT));
     CREATE_TRY(dmalloc(ctx, &ctx->pk_tickets, (size_t)c.n_kv_heads));
-    CREATE_TRY(dmalloc(ctx, &ctx->pk_err, 2));
+    CREATE_TRY(dmalloc(ctx, &ctx->pk_err, 8));
     CREATE_TRY(dmalloc(ctx, &ctx->pk_cand, (size_t)ctx->n_cu));
-    CREATE_TRY(dmalloc(ctx, &ctx->pk_trace, std::max<size_t>((size_t)PK_TRACE_WG * pk_trace_len(c.n_layers),
-                                                             8 * ((size_t)c.n_kv_heads * ctx->nsplit + 4096))));
+    CREATE_TRY(dmalloc(ctx, &ctx->pk_trace, std::max<size_t>(std::max<size_t>((size_t)PK_TRACE_WG * pk_trace_len(c.n_layers),
+                                                             8 * ((size_t)c.n_kv_heads * ctx->nsplit + 4096)),
+                                                             (size_t)se_trace_len(ctx->n_cu, c.n_layers))));
     CREATE_TRY(dmalloc(ctx, &ctx->pk_prompt, (size_t)ctx->pk_prompt_cap));
+    // stream engine: ring slots that fit 160 KiB of LDS beside the control block and the
+    // attention merge area; splits per KV head: one attention item per CU at most
+    ctx->se_nslots = 0;
+    for (int ns = SE_MAXS; ns > SE_DEPTH; ns--)
+        if (se_smem_bytes(ns, ctx->qpk, c.head_dim) <= 160 * 1024) { ctx->se_nslots = ns; break; }
+    ctx->se_max_splits = std::max(1, std::min(64, ctx->n_cu / std::max(1, c.n_kv_heads)));
+    ctx->se_g_words = (size_t)c.dim + c.hidden_dim + (size_t)ctx->q_dim + ctx->n_cu;
+    CREATE_TRY(dmalloc(ctx, &ctx->se_layers, (size_t)c.n_layers));
+    CREATE_TRY(dmalloc(ctx, &ctx->se_g, ctx->se_g_words));
+    CREATE_TRY(dmalloc(ctx, &ctx->se_qcnt, (size_t)c.n_layers * c.n_kv_heads));
+    CREATE_TRY(dmalloc(ctx, &ctx->se_tickets, (size_t)c.n_kv_heads));
+    CREATE_TRY(dmalloc(ctx, &ctx->se_part_o, (size_t)ctx->se_max_splits * c.n_heads * c.head_dim));
+    CREATE_TRY(dmalloc(ctx, &ctx->se_part_ml, (size_t)ctx->se_max_splits * c.n_heads * 2));
     if (hipHostMalloc((void**)&ctx->pk_host, (2 + (size_t)ctx->pk_prompt_cap) * sizeof(int), hipHostMallocDefault) !=
         hipSuccess) {
         g_create_error = "hipHostMalloc failed";
@@ -1124,6 +1269,8 @@ void xh_destroy(xh_ctx* ctx) {
     hipFree(ctx->pf_part); hipFree(ctx->pf_sp); hipFree(ctx->pf_po); hipFree(ctx->pf_pml); hipFree(ctx->pf_cnt); hipFree(ctx->rope_freq);
     hipFree(ctx->pk_layers); hipFree(ctx->pk_counters); hipFree(ctx->pk_tickets); hipFree(ctx->pk_err);
     hipFree(ctx->pk_cand); hipFree(ctx->pk_prompt); hipFree(ctx->pk_trace);
+    hipFree(ctx->se_layers); hipFree(ctx->se_g); hipFree(ctx->se_qcnt); hipFree(ctx->se_tickets);
+    hipFree(ctx->se_part_o); hipFree(ctx->se_part_ml);
     if (ctx->pk_host) hipHostFree(ctx->pk_host);
     for (hipEvent_t e : ctx->pk_ev)
         if (e) hipEventDestroy(e);
@@ -1536,7 +1683,8 @@ int xh_prefill(xh_ctx* ctx, const int* tokens, int n, int pos0, int want_logits,
     HIP_TRY(ctx, hipSetDevice(ctx->dev));
     int rc = check_ready(ctx);
     if (rc) return rc;
-    if (use_persistent(ctx)) {
+    // the stream engine keeps the batched MFMA prompt path where it applies (16x its token loop)
+    if (use_persistent(ctx) && !(ctx->engine == 2 && pf_supported(ctx, n, pos0))) {
         for (int off = 0; off < n && !rc; off += ctx->pk_prompt_cap) {
             const int m = std::min(n - off, ctx->pk_prompt_cap);
             rc = run_persistent(ctx, tokens + off, m, 0, pos0 + off, off + m == n ? want_logits : 0, -1, -1, nullptr);
@@ -1578,7 +1726,7 @@ int xh_perplexity(xh_ctx* ctx, const int* tokens, int n, int pos0, float* probs_
         if ((rc = dmalloc(ctx, &ctx->ppl_tgt, (size_t)m)) || (rc = dmalloc(ctx, &ctx->ppl_prob, (size_t)m))) return rc;
         ctx->ppl_cap = m;
     }
-    if (!use_persistent(ctx) && pf_supported(ctx, m, pos0)) {
+    if ((!use_persistent(ctx) || ctx->engine == 2) && pf_supported(ctx, m, pos0)) {
         rc = prefill_batched(ctx, tokens, m, pos0, 0, tokens + 1, ctx->ppl_prob);
     } else {
         HIP_TRY(ctx, hipMemcpy(ctx->ppl_tgt, tokens + 1, (size_t)m * sizeof(int), hipMemcpyHostToDevice));
@@ -1603,12 +1751,12 @@ int xh_perplexity(xh_ctx* ctx, const int* tokens, int n, int pos0, float* probs_
 }
 
 int xh_set_engine(xh_ctx* ctx, int engine) {
-    if (!ctx || engine < -1 || engine > 1) return XH_E_INVALID;
-    if (engine == 1) {
-        int dt, dtc, ndt;
-        if (!pk_dtypes(ctx, &dt, &dtc, &ndt))
-            return set_err(ctx, XH_E_INVALID, "persistent engine not available for these weights");
-    }
+    if (!ctx || engine < -1 || engine > 2) return XH_E_INVALID;
+    int dt, dtc, ndt;
+    if (engine == 1 && !pk_dtypes(ctx, &dt, &dtc, &ndt))
+        return set_err(ctx, XH_E_INVALID, "persistent engine not available for these weights");
+    if (engine == 2 && !se_supported(ctx, &dt, &dtc, &ndt))
+        return set_err(ctx, XH_E_INVALID, "stream engine not available for these weights");
     ctx->engine = engine;
     return 0;
 }
@@ -1621,7 +1769,8 @@ int xh_last_launch_us(const xh_ctx* ctx, float* us) {
 
 int xh_debug_trace(xh_ctx* ctx, int enable, uint64_t* out, int cap, int* len) {
     if (!ctx) return XH_E_INVALID;
-    const int n = std::max(PK_TRACE_WG * pk_trace_len(ctx->c.n_layers), 8 * (ctx->c.n_kv_heads * ctx->nsplit + 4096));
+    const int n = std::max(std::max(PK_TRACE_WG * pk_trace_len(ctx->c.n_layers), 8 * (ctx->c.n_kv_heads * ctx->nsplit + 4096)),
+                           se_trace_len(ctx->n_cu, ctx->c.n_layers));
     if (len) *len = n;
     if (out && cap > 0) {
         HIP_TRY(ctx, hipSetDevice(ctx->dev));
@@ -1631,6 +1780,7 @@ int xh_debug_trace(xh_ctx* ctx, int enable, uint64_t* out, int cap, int* len) {
         ctx->pk_trace_on = (enable & 1) != 0;
         ctx->aw_trace_on = (enable & 2) != 0;
         ctx->qaw_trace_on = (enable & 4) != 0;
+        ctx->se_trace_on = (enable & 8) != 0;
         drop_graphs(ctx);
         HIP_TRY(ctx, hipMemset(ctx->pk_trace, 0, (size_t)n * sizeof(uint64_t)));
     }
@@ -1652,7 +1802,7 @@ int xh_get_option(const xh_ctx* ctx, int option, int* value) {
 
 int xh_get_engine(const xh_ctx* ctx) {
     if (!ctx) return -1;
-    return use_persistent(const_cast<xh_ctx*>(ctx)) ? 1 : 0;
+    return use_persistent(const_cast<xh_ctx*>(ctx)) ? ctx->engine : 0;
 }
 
 int xh_set_option(xh_ctx* ctx, int option, int value) {

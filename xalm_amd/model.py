@@ -105,7 +105,7 @@ class Model:
         L.check(L.lib().xh_perplexity(self._ctx, L.ptr(toks), int(toks.size), int(pos0), L.ptr(out)), self._ctx)
         return out[: toks.size - 1]
 
-    # engine: 0 = hipGraph of kernels per token, 1 = persistent kernel, -1 = automatic
+    # engine: 0 = hipGraph of kernels per token, 1 = persistent kernel, 2 = stream kernel, -1 = automatic
     ENGINE_GRAPH, ENGINE_PERSISTENT, ENGINE_AUTO = 0, 1, -1
 
     def set_engine(self, engine: int):
