@@ -128,6 +128,71 @@ __global__ __launch_bounds__(512) void reg_kernel(const char* buf, size_t per_cu
     if (acc == 123.456f) sink[blockIdx.x] = 1;
 }
 
+// KV-cache access patterns of long-context attention (rows of 2 KiB = 8 heads x 256 B), register
+// loads, 1024-thread workgroups, one round = 4 loads of 16 B per thread.
+//   HEADS=1 : workgroup (head g = b % 8, split b / 8) reads 256 B of each of its rows (today)
+//   HEADS=8 : workgroup (split b) reads whole 2 KiB rows
+//   PIPE    : rounds in flight (1 = load, wait, next; 2 = next round requested before the wait)
+template <int HEADS, int PIPE>
+__global__ __launch_bounds__(1024) void kv_kernel(const char* kv, int rows_per_wg, unsigned long long* sink) {
+    typedef unsigned u4 __attribute__((ext_vector_type(4)));
+    const int tid = threadIdx.x;
+    const int lpr = 16 * HEADS;             // lanes per row
+    const int rpp = 1024 / lpr;             // rows per pass
+    const int g = HEADS == 1 ? blockIdx.x % 8 : 0;
+    const int split = HEADS == 1 ? blockIdx.x / 8 : blockIdx.x;
+    const size_t row0 = (size_t)split * rows_per_wg;
+    const int sub = tid % lpr, rr = tid / lpr;
+    const char* base = kv + row0 * 2048 + g * 256 + sub * 16;
+    float acc = 0.f;
+    const int rounds = rows_per_wg / (4 * rpp);
+    u4 cur[4], nxt[4];
+    auto load = [&](u4 (&v)[4], int r) {
+#pragma unroll
+        for (int p = 0; p < 4; p++) {
+            const size_t row = (size_t)r * 4 * rpp + p * rpp + rr;
+            v[p] = *(const __attribute__((address_space(1))) u4*)(base + row * 2048);
+        }
+    };
+    if (PIPE == 1) {
+        for (int r = 0; r < rounds; r++) {
+            load(cur, r);
+#pragma unroll
+            for (int p = 0; p < 4; p++) acc += __builtin_bit_cast(float, cur[p].x);
+        }
+    } else {
+        load(cur, 0);
+        for (int r = 0; r < rounds; r++) {
+            if (r + 1 < rounds) load(nxt, r + 1);
+#pragma unroll
+            for (int p = 0; p < 4; p++) acc += __builtin_bit_cast(float, cur[p].x);
+#pragma unroll
+            for (int p = 0; p < 4; p++) cur[p] = nxt[p];
+        }
+    }
+    if (acc == 123.456f) sink[blockIdx.x] = 1;
+}
+
+template <int HEADS, int PIPE>
+void run_kv(const char* kv, size_t bytes, int ncu, int wg_per_cu, unsigned long long* sink) {
+    const int nwg = ncu * wg_per_cu;
+    const size_t rows = bytes / 2048;
+    const int rows_per_wg = (int)(rows * (HEADS == 1 ? 8 : 1) / nwg);
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    auto k = kv_kernel<HEADS, PIPE>;
+    for (int it = 0; it < 2; it++) hipLaunchKernelGGL(k, dim3(nwg), dim3(1024), 0, 0, kv, rows_per_wg, sink);
+    hipEventRecord(e0);
+    for (int it = 0; it < 5; it++) hipLaunchKernelGGL(k, dim3(nwg), dim3(1024), 0, 0, kv, rows_per_wg, sink);
+    hipEventRecord(e1);
+    hipEventSynchronize(e1);
+    float ms = 0;
+    hipEventElapsedTime(&ms, e0, e1);
+    printf("kv pattern heads/wg=%d rounds in flight=%d wg/cu=%d rows/wg=%5d : %7.1f GB/s (%.1f us)\n", HEADS, PIPE,
+           wg_per_cu, rows_per_wg, (double)bytes * 5 / (ms * 1e-3) / 1e9, ms * 1000 / 5);
+}
+
 template <int NL, int NC, int DEPTH, int PAT, bool NT>
 void run(const char* buf, size_t per_cu, int ncu, unsigned long long* sink, const char* name) {
     auto k = ring_kernel<NL, NC, DEPTH, PAT, NT>;
@@ -175,6 +240,15 @@ int main() {
         hipEventElapsedTime(&ms, e0, e1);
         printf("%-44s : %7.1f GB/s\n", "register nt loads, 16 waves/CU x 4 KiB", (double)per_cu * ncu * 5 / (ms * 1e-3) / 1e9);
     }
+    // one 32k-context layer: K (or V) ring = 32768 rows x 2 KiB = 64 MiB; 128 MiB = K and V
+    const size_t kvb = (size_t)128 << 20;
+    run_kv<1, 1>(buf, kvb, ncu, 1, sink);
+    run_kv<1, 2>(buf, kvb, ncu, 1, sink);
+    run_kv<1, 1>(buf, kvb, ncu, 2, sink);
+    run_kv<1, 2>(buf, kvb, ncu, 2, sink);
+    run_kv<8, 1>(buf, kvb, ncu, 1, sink);
+    run_kv<8, 2>(buf, kvb, ncu, 1, sink);
+    run_kv<8, 2>(buf, kvb, ncu, 2, sink);
     run<1, 7, 3, 1, true>(buf, per_cu, ncu, sink, "ring, strided tiles (stream engine today)");
     run<1, 7, 3, 0, true>(buf, per_cu, ncu, sink, "ring, contiguous slots");
     run<1, 7, 2, 1, true>(buf, per_cu, ncu, sink, "ring, strided, depth 2");

@@ -175,22 +175,36 @@ __device__ __forceinline__ void attn_block(const AttnArgs& a, const int g, const
             if (sub == 0) sc[h * T + (t - t0)] = p * scale;
         }
     };
+    // rounds of RPP * ATTN_PREF rows, software-pipelined: round r + 1 is requested before round
+    // r's dot products.  Two named register sets alternate (unrolled by two): a copy of a
+    // register with a load in flight would make the compiler wait for that load, and a load
+    // behind a branch would merge into a vmcnt(0); the last round has its own block, so every
+    // wait is counted.  (One round in flight per wave left the passes latency-bound at long
+    // contexts.)
+    constexpr int STEP = ATTN_PREF * RPP;
+    auto ld_round = [&](u32x4 (&v)[ATTN_PREF], const uint16_t* base_p, const int base) {
 #pragma unroll
-    for (int p = 0; p < ATTN_PREF; p++) {
-        const int t = t0 + rr + p * RPP;
-        if (t < t1) score_row(kr[p], t);
-    }
-    for (int base = t0 + ATTN_PREF * RPP; base < t1; base += ATTN_PREF * RPP) {
-        u32x4 kk[ATTN_PREF];
+        for (int p = 0; p < ATTN_PREF; p++) v[p] = ld_kv(base_p, min(base + rr + p * RPP, t1 - 1));
+    };
+    auto score_round = [&](const u32x4 (&v)[ATTN_PREF], const int base) {
 #pragma unroll
         for (int p = 0; p < ATTN_PREF; p++) {
             const int t = base + rr + p * RPP;
-            if (t < t1) kk[p] = ld_kv(a.kc, t);
+            if (t < t1) score_row(v[p], t);
         }
-#pragma unroll
-        for (int p = 0; p < ATTN_PREF; p++) {
-            const int t = base + rr + p * RPP;
-            if (t < t1) score_row(kk[p], t);
+    };
+    {
+        u32x4 rb[ATTN_PREF];
+        int base = t0;
+        for (;;) {
+            if (base + STEP >= t1) { score_round(kr, base); break; }
+            ld_round(rb, a.kc, base + STEP);
+            score_round(kr, base);
+            base += STEP;
+            if (base + STEP >= t1) { score_round(rb, base); break; }
+            ld_round(kr, a.kc, base + STEP);
+            score_round(rb, base);
+            base += STEP;
         }
     }
     __syncthreads();
@@ -230,22 +244,25 @@ __device__ __forceinline__ void attn_block(const AttnArgs& a, const int g, const
             for (int i = 0; i < 8; i++) acc[h][i] = fmaf(e, vf[i], acc[h][i]);
         }
     };
+    {
+        auto pv_round = [&](const u32x4 (&v)[ATTN_PREF], const int base) {
 #pragma unroll
-    for (int p = 0; p < ATTN_PREF; p++) {
-        const int t = t0 + rr + p * RPP;
-        if (t < t1) pv_row(vr[p], t);
-    }
-    for (int base = t0 + ATTN_PREF * RPP; base < t1; base += ATTN_PREF * RPP) {
-        u32x4 vv[ATTN_PREF];
-#pragma unroll
-        for (int p = 0; p < ATTN_PREF; p++) {
-            const int t = base + rr + p * RPP;
-            if (t < t1) vv[p] = ld_kv(a.vc, t);
-        }
-#pragma unroll
-        for (int p = 0; p < ATTN_PREF; p++) {
-            const int t = base + rr + p * RPP;
-            if (t < t1) pv_row(vv[p], t);
+            for (int p = 0; p < ATTN_PREF; p++) {
+                const int t = base + rr + p * RPP;
+                if (t < t1) pv_row(v[p], t);
+            }
+        };
+        u32x4 rb[ATTN_PREF];
+        int base = t0;
+        for (;;) {
+            if (base + STEP >= t1) { pv_round(vr, base); break; }
+            ld_round(rb, a.vc, base + STEP);
+            pv_round(vr, base);
+            base += STEP;
+            if (base + STEP >= t1) { pv_round(rb, base); break; }
+            ld_round(vr, a.vc, base + STEP);
+            pv_round(rb, base);
+            base += STEP;
         }
     }
     ATTN_STAMP(7);

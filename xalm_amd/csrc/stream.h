@@ -88,6 +88,8 @@ struct SeArgs {
     int split_rows;            // attention rows per split (target)
     int max_splits;            // splits per KV head (<= n_cu / n_kv_heads)
     int rotate;                // 1: CU b streams a tile's K-steps from b % nk on (else from 0)
+    int debug;                 // experiments (results invalid): 1 no FMA, 2 no hand-off waits, 4 no tile combine,
+                               // 8 no per-slot loader stamps in the trace
     int* err;                  // [0] timeout flag
     // work of this launch
     const int* prompt;
@@ -304,10 +306,11 @@ __device__ __forceinline__ void se_loader(const SeArgs& a, char* ring, SeCtl* c,
     uint64_t i0 = 0, i1 = 0, i2 = 0, i3 = 0;             // debug: issue times of the FIFO entries
     uint64_t tr_lat = 0, tr_cnt = 0, tr_blk = 0;
     auto publish_oldest = [&]() {
-        const uint64_t tb = a.trace ? se_now() : 0;
+        const bool stamp = a.trace && !(a.debug & 8);
+        const uint64_t tb = stamp ? se_now() : 0;
         se_vmcnt_le((nfl > 1 ? n1 : 0) + (nfl > 2 ? n2 : 0) + (nfl > 3 ? n3 : 0));
         vstore(&c->full[s0 % ns], s0);
-        if (a.trace) {
+        if (stamp) {
             const uint64_t now = se_now();
             tr_blk += now - tb;
             tr_lat += now - i0;
@@ -379,7 +382,7 @@ __device__ __forceinline__ void se_loader(const SeArgs& a, char* ring, SeCtl* c,
                     const uint32_t dst = ring_lds + (uint32_t)slot * SE_SLOT;
                     for (int p = 0; p < TH; p++)
                         se_glds(src + (size_t)p * m.rb + (size_t)ks * 1024, __builtin_amdgcn_readfirstlane(dst + p * 1024));
-                    const uint64_t ti = a.trace ? se_now() : 0;
+                    const uint64_t ti = (a.trace && !(a.debug & 8)) ? se_now() : 0;
                     if (nfl == 0) { s0 = seq; n0 = TH; i0 = ti; }
                     else if (nfl == 1) { s1 = seq; n1 = TH; i1 = ti; }
                     else if (nfl == 2) { s2 = seq; n2 = TH; i2 = ti; }
@@ -645,12 +648,16 @@ __device__ __forceinline__ bool se_matrix(const SeArgs& a, SeCtl* c, const char*
                     for (int p = 0; p < 16; p++) w[p] = *(const u32x4*)(sp + p * 1024);
                     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                     if (lane == 0) vstore(&c->free_[slot], s);
+                    if (!(a.debug & 1)) {
 #pragma unroll
-                    for (int p = 0; p < 16; p++) acc[p] = se_dot16<DT>(w[p], xr, acc[p]);
+                        for (int p = 0; p < 16; p++) acc[p] = se_dot16<DT>(w[p], xr, acc[p]);
+                    } else {
+                        acc[0] += __builtin_bit_cast(float, w[0].x & 1u);
+                    }
                 }
                 se_rotate<E>(xr);
             }
-            if (!se_tile_end<HD, QPK>(a, c, st, tk, l, ph, acc, P, t0, t1 - t0)) return false;
+            if (!(a.debug & 4) && !se_tile_end<HD, QPK>(a, c, st, tk, l, ph, acc, P, t0, t1 - t0)) return false;
         }
         st.seq += m.nk;
         st.tile++;
@@ -683,7 +690,7 @@ __device__ __forceinline__ bool se_sweep(const SeArgs& a, SeCtl* c, const SeStat
                 ok = ok && u.y == tag && u.w == tag;
             }
         }
-        if (__all(ok)) break;
+        if (__all(ok) || (a.debug & 2)) break;
         __builtin_amdgcn_s_sleep(1);
         if (!sp.step(a, c)) return false;
     }
@@ -1052,7 +1059,7 @@ __global__ __launch_bounds__(SE_THREADS) void stream_decode_kernel(const SeArgs 
                 normw = a.layers[l].attn_norm;
             } else if (ph == SE_WO) {
                 // attention (src/infer.cpp:434-444) on the CUs that own a (head, split) item
-                if (b < a.n_kv_heads * S && wid < SE_NA) {
+                if (b < a.n_kv_heads * S && wid < SE_NA && !(a.debug & 2)) {
                     if (!se_attention<HD, QPK>(a, c, att, st, l, t, b / S, b % S, S, T, kv_sink, kv_len,
                                                trp ? trp + q * SE_TR_PH : nullptr))
                         return;
@@ -1119,7 +1126,7 @@ __global__ __launch_bounds__(SE_THREADS) void stream_decode_kernel(const SeArgs 
                     ok = ok && (unsigned)(k & 0x7FFF) == tk.ctag;
                     bb = k > bb ? k : bb;
                 }
-                if (__all(ok)) { best = bb; break; }
+                if (__all(ok) || (a.debug & 2)) { best = bb; break; }
                 __builtin_amdgcn_s_sleep(1);
                 if (!sp.step(a, c)) return;
             }
@@ -1129,6 +1136,7 @@ __global__ __launch_bounds__(SE_THREADS) void stream_decode_kernel(const SeArgs 
                 best = other > best ? other : best;
             }
             token = (best >> 15) ? 0x1FFFF - (int)((best >> 15) & 0x1FFFF) : 0;
+            if (token >= a.vocab) token = 0;  // only reachable with the debug switches
         }
     }
     // consumers done: release the loader if it still waits for ring slots

@@ -713,6 +713,8 @@ int run_stream(xh_ctx* ctx, const int* prompt, int n_prompt, int n_gen, int pos0
     {
         const char* ev = getenv("XALM_SE_ROTATE");  // experiment switch (default on)
         a.rotate = ev ? atoi(ev) : 1;
+        const char* dv = getenv("XALM_SE_DEBUG");   // experiments only: results invalid
+        a.debug = dv ? atoi(dv) : 0;
     }
     a.err = ctx->pk_err;
     a.prompt = ctx->pk_prompt; a.n_prompt = n_prompt; a.n_gen = n_gen; a.pos0 = pos0; a.logits_last = logits_last;
