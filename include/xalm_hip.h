@@ -200,7 +200,11 @@ int xh_set_graphs(xh_ctx* ctx, int enable);
  * mantissa; measured faster there); 2 = split-f16 wherever the weights convert exactly to
  * f16 (f16, fp8); 3 = f32-input MFMA only; 0 = one forward per token (the reference's loop,
  * src/main.cpp:94-100).  Same math per token up to f32 rounding. */
-enum xh_option { XH_OPT_FUSE_ATTN_WO = 1, XH_OPT_PREFILL = 2 };
+/* XH_OPT_PREFILL_GLU_SPLIT (default 1): where the W2 GEMM takes split-f16 input, the GLU
+ * epilogue of the W1/W3 GEMM writes those f16 hi/lo fragments directly (one launch); 0 = GLU to
+ * f32 first, then split in the W2 GEMM's input pass (two launches).  Bit-identical results; a
+ * debug knob so tests cover both routes. */
+enum xh_option { XH_OPT_FUSE_ATTN_WO = 1, XH_OPT_PREFILL = 2, XH_OPT_PREFILL_GLU_SPLIT = 3 };
 int xh_set_option(xh_ctx* ctx, int option, int value);
 int xh_get_option(const xh_ctx* ctx, int option, int* value);
 

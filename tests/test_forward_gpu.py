@@ -202,13 +202,16 @@ def synthetic_pair(wdt, dim=256, hidden=512, n_layers=2, vocab=512, context=256)
     return gm, om
 
 
+@pytest.mark.parametrize("glu", [1, 0])
 @pytest.mark.parametrize("mode", [1, 2, 3])
 @pytest.mark.parametrize("wdt", [L.F16, L.F8_E4M3, L.F8_E5M2])
-def test_prefill_gemm_paths_on_synthetic_weights(wdt, mode):
+def test_prefill_gemm_paths_on_synthetic_weights(wdt, mode, glu):
     # dims (256 / 512) that take the split-f16 kernel for fp8 too (K % 8E); 100 tokens = a full
-    # pass and a partial one; logits vs the oracle's token loop, then the perplexity path
+    # pass and a partial one; logits vs the oracle's token loop, then the perplexity path.
+    # glu 0 routes the W2 input through the f32 GLU epilogue + split pass instead of the fused one
     gm, om = synthetic_pair(wdt)
     gm.set_option(L.OPT_PREFILL, mode)
+    gm.set_option(L.OPT_PREFILL_GLU_SPLIT, glu)
     toks = [1] + [3 + (i * 37) % 500 for i in range(99)]
     st = InferenceState(gm.config)
     gm.prefill(toks, 0, st)
@@ -219,7 +222,24 @@ def test_prefill_gemm_paths_on_synthetic_weights(wdt, mode):
     assert np.abs(st.logits() - ref).max() <= tol(ref), float(np.abs(st.logits() - ref).max())
     gm2, om2 = synthetic_pair(wdt)
     gm2.set_option(L.OPT_PREFILL, mode)
+    gm2.set_option(L.OPT_PREFILL_GLU_SPLIT, glu)
     check_probs(gm2.token_probs(toks[:70]), om2, toks[:70])
+
+
+@pytest.mark.parametrize("wdt", [L.F16, L.F8_E4M3])
+def test_fused_glu_split_is_bit_identical(wdt):
+    # the fused GLU -> split-f16 epilogue and the two-launch route produce the same W2 input
+    toks = [1] + [3 + (i * 41) % 500 for i in range(99)]
+    out = []
+    for glu in (1, 0):
+        gm, _ = synthetic_pair(wdt)
+        gm.set_option(L.OPT_PREFILL, 2)
+        gm.set_option(L.OPT_PREFILL_GLU_SPLIT, glu)
+        assert gm.get_option(L.OPT_PREFILL_GLU_SPLIT) == glu
+        st = InferenceState(gm.config)
+        gm.prefill(toks, 0, st)
+        out.append(st.logits().copy())
+    assert np.array_equal(out[0], out[1]), float(np.abs(out[0] - out[1]).max())
 
 
 @pytest.mark.parametrize("batched", [1, 2, 3])

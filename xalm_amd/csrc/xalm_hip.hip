@@ -120,6 +120,7 @@ struct xh_ctx {
     // 2 = split-f16 wherever the weights convert exactly; 3 = f32 MFMA only
     int prefill_gemm = 1;
     bool pf_split_ready = false;                 // pf_norm left the next GEMM's split input
+    bool pf_glu_split = true;                    // XH_OPT_PREFILL_GLU_SPLIT: fused GLU -> split input
     bool pf_alloc = false;
     uint16_t *pf_xh = nullptr, *pf_xl = nullptr; // [PF_TOK][max K] f16 halves of a GEMM input
     float* pf_xs = nullptr;                      // [PF_TOK] 1 / row scale
@@ -199,6 +200,24 @@ int set_err(xh_ctx* ctx, int code, const char* fmt, ...) {
             return set_err((ctx), XH_E_HIP, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(_e), \
                            __FILE__, __LINE__);                                                \
     } while (0)
+
+// Host <-> device copies and fills go on ctx->stream and wait for it.  ctx->stream is
+// non-blocking, so null-stream work (hipMemcpy, hipMemset, hipMemcpy2D) is not ordered with
+// its kernels: a fill can land after a kernel wrote the buffer, and a pageable upload can
+// return before its DMA does.
+hipError_t copy_sync(xh_ctx* ctx, void* dst, const void* src, size_t bytes, hipMemcpyKind kind) {
+    const hipError_t e = hipMemcpyAsync(dst, src, bytes, kind, ctx->stream);
+    return e != hipSuccess ? e : hipStreamSynchronize(ctx->stream);
+}
+hipError_t copy2d_sync(xh_ctx* ctx, void* dst, size_t dpitch, const void* src, size_t spitch, size_t width,
+                       size_t height) {
+    const hipError_t e = hipMemcpy2DAsync(dst, dpitch, src, spitch, width, height, hipMemcpyHostToDevice, ctx->stream);
+    return e != hipSuccess ? e : hipStreamSynchronize(ctx->stream);
+}
+hipError_t fill_sync(xh_ctx* ctx, void* dst, int value, size_t bytes) {
+    const hipError_t e = hipMemsetAsync(dst, value, bytes, ctx->stream);
+    return e != hipSuccess ? e : hipStreamSynchronize(ctx->stream);
+}
 
 // ---------------------------------------------------------------------------------------
 // gemv launch dispatch
@@ -448,12 +467,12 @@ int launch_qaw(xh_ctx* ctx, int l, hipStream_t s) {
 int check_aw(xh_ctx* ctx) {
     {
         int e = 0;
-        HIP_TRY(ctx, hipMemcpy(&e, qaw_err(ctx), sizeof(int), hipMemcpyDeviceToHost));
+        HIP_TRY(ctx, copy_sync(ctx, &e, qaw_err(ctx), sizeof(int), hipMemcpyDeviceToHost));
         if (e) return set_err(ctx, XH_E_HIP, "qkv -> attention -> Wo hand-off timed out");
     }
     if (!ctx->fuse_attn_wo) return 0;
     std::vector<unsigned> h((size_t)ctx->c.n_layers * AW_SYNC_WORDS);
-    HIP_TRY(ctx, hipMemcpy(h.data(), ctx->aw_sync, h.size() * sizeof(unsigned), hipMemcpyDeviceToHost));
+    HIP_TRY(ctx, copy_sync(ctx, h.data(), ctx->aw_sync, h.size() * sizeof(unsigned), hipMemcpyDeviceToHost));
     for (int l = 0; l < ctx->c.n_layers; l++)
         if (h[(size_t)AW_SYNC_WORDS * l + 2]) return set_err(ctx, XH_E_HIP, "layer %d: attention -> Wo hand-off timed out", l);
     return 0;
@@ -594,7 +613,7 @@ int run_persistent(xh_ctx* ctx, const int* prompt, int n_prompt, int n_gen, int 
             const LayerW& w = ctx->L[l];
             h[l] = PkLayer{w.wqkv, w.wo, w.w13, w.w2, w.attn_norm, w.ffn_norm, ctx->kcache(l), ctx->vcache(l)};
         }
-        HIP_TRY(ctx, hipMemcpy(ctx->pk_layers, h.data(), h.size() * sizeof(PkLayer), hipMemcpyHostToDevice));
+        HIP_TRY(ctx, copy_sync(ctx, ctx->pk_layers, h.data(), h.size() * sizeof(PkLayer), hipMemcpyHostToDevice));
         ctx->pk_layers_dirty = false;
     }
     if (n_prompt) {
@@ -680,7 +699,7 @@ int run_stream(xh_ctx* ctx, const int* prompt, int n_prompt, int n_gen, int pos0
             const LayerW& w = ctx->L[l];
             h[l] = SeLayer{w.wqkv, w.wo, w.w13, w.w2, w.attn_norm, w.ffn_norm, ctx->kcache(l), ctx->vcache(l)};
         }
-        HIP_TRY(ctx, hipMemcpy(ctx->se_layers, h.data(), h.size() * sizeof(SeLayer), hipMemcpyHostToDevice));
+        HIP_TRY(ctx, copy_sync(ctx, ctx->se_layers, h.data(), h.size() * sizeof(SeLayer), hipMemcpyHostToDevice));
         ctx->se_layers_dirty = false;
     }
     if (n_prompt) {
@@ -740,7 +759,7 @@ int run_stream(xh_ctx* ctx, const int* prompt, int n_prompt, int n_gen, int pos0
     ctx->pk_last_us = ms * 1000.f;
     if (ctx->pk_host[0]) {
         int info[4] = {0, 0, 0, 0};
-        hipMemcpy(info, ctx->pk_err + 2, sizeof info, hipMemcpyDeviceToHost);
+        copy_sync(ctx, info, ctx->pk_err + 2, sizeof info, hipMemcpyDeviceToHost);
         return set_err(ctx, XH_E_HIP, "stream kernel: a wait timed out (2 s): code %d workgroup %d wave %d value %d",
                        info[0], info[1], info[2], info[3]);
     }
@@ -1036,13 +1055,18 @@ int prefill_batched(xh_ctx* ctx, const int* tokens, int n, int pos0, int want_lo
             ks = pf_gemm(ctx, kdt(w.w13_dt, w.w13_x), w.w13, c.dim, 2 * c.hidden_dim, ctx->pf_xn, m);
             if (!ks) return set_err(ctx, XH_E_INVALID, "prefill: w1/w3 shape not supported");
             const int E2 = pf_split_E(ctx, kdt(w.w2_dt, w.w2_x), c.hidden_dim, c.dim);
-            if (E2 && (size_t)c.hidden_dim * sizeof(float) <= 64 * 1024) {
+            // dynamic LDS = one f32 row of h; the kernel adds a static 16-float reduction array
+            const size_t glu_lds = (size_t)c.hidden_dim * sizeof(float);
+            bool glu_fused = false;
+            if (E2 && ctx->pf_glu_split && glu_lds + 16 * sizeof(float) <= 64 * 1024) {
                 // GLU epilogue straight into the W2 GEMM's split-f16 fragments (one launch)
                 hipLaunchKernelGGL(prefill_glu_split_kernel, dim3(32 * ((m + 31) / 32)), dim3(1024),
-                                   (size_t)c.hidden_dim * sizeof(float), ctx->stream, (const float*)ctx->pf_part, ks,
+                                   glu_lds, ctx->stream, (const float*)ctx->pf_part, ks,
                                    m, c.hidden_dim, c.act, E2, ctx->pf_xh, ctx->pf_xl, ctx->pf_xs);
-                ctx->pf_split_ready = true;
-            } else {
+                glu_fused = hipGetLastError() == hipSuccess;  // a refused launch takes the two-launch path
+                ctx->pf_split_ready = glu_fused;
+            }
+            if (!glu_fused) {
                 e = PfEpiArgs{};
                 e.ks = ks; e.n = m; e.rows = 2 * c.hidden_dim; e.epi = EPI_GLU; e.out = ctx->pf_h; e.act = c.act;
                 pf_epi(ctx, e);
@@ -1098,7 +1122,7 @@ int prefill_batched(xh_ctx* ctx, const int* tokens, int n, int pos0, int want_lo
 template <typename T>
 int dmalloc(xh_ctx* ctx, T** p, size_t n) {
     HIP_TRY(ctx, hipMalloc((void**)p, n ? n * sizeof(T) : 16));
-    HIP_TRY(ctx, hipMemset(*p, 0, n ? n * sizeof(T) : 16));
+    HIP_TRY(ctx, fill_sync(ctx, *p, 0, n ? n * sizeof(T) : 16));
     return 0;
 }
 
@@ -1240,10 +1264,10 @@ int xh_create(const xh_config* cfg, int device_ordinal, xh_ctx** out) {
         sc[j / 2] = cosf(val);
         sn[j / 2] = sinf(val);
     }
-    if (hipMemcpy(ctx->rope_freq, fr.data(), fr.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(ctx->sink_cos, sc.data(), sc.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(ctx->sink_sin, sn.data(), sn.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(ctx->sp, ctx->sp_host, sizeof(StepParams), hipMemcpyHostToDevice) != hipSuccess) {
+    if (copy_sync(ctx, ctx->rope_freq, fr.data(), fr.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+        copy_sync(ctx, ctx->sink_cos, sc.data(), sc.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+        copy_sync(ctx, ctx->sink_sin, sn.data(), sn.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+        copy_sync(ctx, ctx->sp, ctx->sp_host, sizeof(StepParams), hipMemcpyHostToDevice) != hipSuccess) {
         g_create_error = "initial copies failed";
         xh_destroy(ctx);
         return XH_E_HIP;
@@ -1459,8 +1483,8 @@ int xh_upload(xh_ctx* ctx, int kind, int layer, int dtype, const void* host, siz
     int rc = check_bytes(ctx, kind, dtype, bytes);
     if (!rc) rc = tensor_slot(ctx, kind, layer, dtype, &s);
     if (rc) return rc;
-    HIP_TRY(ctx, hipMemcpy2D(s.base, s.pitch, host, s.cols * dtype_size(dtype), s.cols * dtype_size(dtype), s.rows,
-                             hipMemcpyHostToDevice));
+    HIP_TRY(ctx, copy2d_sync(ctx, s.base, s.pitch, host, s.cols * dtype_size(dtype), s.cols * dtype_size(dtype),
+                                 s.rows));
     return scan_f8(ctx, kind, layer, dtype, s);
 }
 
@@ -1495,8 +1519,8 @@ int xh_upload_file(xh_ctx* ctx, int kind, int layer, int dtype, const char* path
         const size_t row_bytes = s.cols * dtype_size(dtype);
         // unregistered (e.g. a mapping the driver cannot pin) the same copy runs pageable
         const bool reg = hipHostRegister(map, len, hipHostRegisterReadOnly) == hipSuccess;
-        const hipError_t e = hipMemcpy2D(s.base, s.pitch, (const char*)map + (offset - a0), row_bytes, row_bytes,
-                                         s.rows, hipMemcpyHostToDevice);
+        const hipError_t e = copy2d_sync(ctx, s.base, s.pitch, (const char*)map + (offset - a0), row_bytes,
+                                         row_bytes, s.rows);
         if (reg) hipHostUnregister(map);
         if (e != hipSuccess) rc = set_err(ctx, XH_E_HIP, "%s: copy to the device: %s", path, hipGetErrorString(e));
     }
@@ -1568,7 +1592,7 @@ int xh_decode_greedy(xh_ctx* ctx, int pos, int n_steps, int stop_a, int stop_b, 
         if (done) rc = host_step_params(ctx, 0, pos + done - 1);
         if (rc) return rc;
         if (tokens_out && done)
-            HIP_TRY(ctx, hipMemcpy(tokens_out, ctx->dec_tokens, (size_t)done * sizeof(int), hipMemcpyDeviceToHost));
+            HIP_TRY(ctx, copy_sync(ctx, tokens_out, ctx->dec_tokens, (size_t)done * sizeof(int), hipMemcpyDeviceToHost));
         if (n_done) *n_done = done;
         return 0;
     }
@@ -1642,7 +1666,7 @@ int xh_kv_write(xh_ctx* ctx, int layer, int which, int slot0, int n_slots, const
         return set_err(ctx, XH_E_INVALID, "bad kv_write arguments");
     HIP_TRY(ctx, hipSetDevice(ctx->dev));
     uint16_t* base = (which ? ctx->vcache(layer) : ctx->kcache(layer)) + (size_t)slot0 * ctx->kv_dim;
-    HIP_TRY(ctx, hipMemcpy(base, host, (size_t)n_slots * ctx->kv_dim * 2, hipMemcpyHostToDevice));
+    HIP_TRY(ctx, copy_sync(ctx, base, host, (size_t)n_slots * ctx->kv_dim * 2, hipMemcpyHostToDevice));
     return 0;
 }
 
@@ -1653,7 +1677,7 @@ int xh_kv_read(xh_ctx* ctx, int layer, int which, int slot0, int n_slots, uint16
     HIP_TRY(ctx, hipSetDevice(ctx->dev));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     const uint16_t* base = (which ? ctx->vcache(layer) : ctx->kcache(layer)) + (size_t)slot0 * ctx->kv_dim;
-    HIP_TRY(ctx, hipMemcpy(host, base, (size_t)n_slots * ctx->kv_dim * 2, hipMemcpyDeviceToHost));
+    HIP_TRY(ctx, copy_sync(ctx, host, base, (size_t)n_slots * ctx->kv_dim * 2, hipMemcpyDeviceToHost));
     return 0;
 }
 
@@ -1731,7 +1755,7 @@ int xh_perplexity(xh_ctx* ctx, const int* tokens, int n, int pos0, float* probs_
     if ((!use_persistent(ctx) || ctx->engine == 2) && pf_supported(ctx, m, pos0)) {
         rc = prefill_batched(ctx, tokens, m, pos0, 0, tokens + 1, ctx->ppl_prob);
     } else {
-        HIP_TRY(ctx, hipMemcpy(ctx->ppl_tgt, tokens + 1, (size_t)m * sizeof(int), hipMemcpyHostToDevice));
+        HIP_TRY(ctx, copy_sync(ctx, ctx->ppl_tgt, tokens + 1, (size_t)m * sizeof(int), hipMemcpyHostToDevice));
         for (int i = 0; i < m && !rc; i++) {
             if (use_persistent(ctx)) {
                 rc = run_persistent(ctx, tokens + i, 1, 0, pos0 + i, 1, -1, -1, nullptr);
@@ -1776,7 +1800,7 @@ int xh_debug_trace(xh_ctx* ctx, int enable, uint64_t* out, int cap, int* len) {
     if (len) *len = n;
     if (out && cap > 0) {
         HIP_TRY(ctx, hipSetDevice(ctx->dev));
-        HIP_TRY(ctx, hipMemcpy(out, ctx->pk_trace, (size_t)std::min(cap, n) * sizeof(uint64_t), hipMemcpyDeviceToHost));
+        HIP_TRY(ctx, copy_sync(ctx, out, ctx->pk_trace, (size_t)std::min(cap, n) * sizeof(uint64_t), hipMemcpyDeviceToHost));
     }
     if (enable >= 0) {
         ctx->pk_trace_on = (enable & 1) != 0;
@@ -1784,7 +1808,7 @@ int xh_debug_trace(xh_ctx* ctx, int enable, uint64_t* out, int cap, int* len) {
         ctx->qaw_trace_on = (enable & 4) != 0;
         ctx->se_trace_on = (enable & 8) != 0;
         drop_graphs(ctx);
-        HIP_TRY(ctx, hipMemset(ctx->pk_trace, 0, (size_t)n * sizeof(uint64_t)));
+        HIP_TRY(ctx, fill_sync(ctx, ctx->pk_trace, 0, (size_t)n * sizeof(uint64_t)));
     }
     return 0;
 }
@@ -1798,6 +1822,7 @@ int xh_get_option(const xh_ctx* ctx, int option, int* value) {
                      : ctx->fuse_attn_wo ? 1 : 0;
             return 0;
         case XH_OPT_PREFILL: *value = ctx->prefill_batched ? ctx->prefill_gemm : 0; return 0;
+        case XH_OPT_PREFILL_GLU_SPLIT: *value = ctx->pf_glu_split ? 1 : 0; return 0;
         default: return XH_E_INVALID;
     }
 }
@@ -1820,6 +1845,10 @@ int xh_set_option(xh_ctx* ctx, int option, int value) {
             if (value < 0 || value > 3) return set_err(ctx, XH_E_INVALID, "XH_OPT_PREFILL: 0 ... 3");
             ctx->prefill_batched = value != 0;
             if (value) ctx->prefill_gemm = value;
+            return 0;
+        case XH_OPT_PREFILL_GLU_SPLIT:
+            if (value < 0 || value > 1) return set_err(ctx, XH_E_INVALID, "XH_OPT_PREFILL_GLU_SPLIT: 0 or 1");
+            ctx->pf_glu_split = value != 0;
             return 0;
         default: return set_err(ctx, XH_E_INVALID, "unknown option %d", option);
     }
