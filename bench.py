@@ -188,6 +188,9 @@ def main():
                     help="also time xh_prefill of this many prompt tokens (batched f32-MFMA path; 0 = skip)")
     ap.add_argument("--fuse-attn-wo", type=int, default=1, choices=(0, 1, 2),
                     help="graph engine: qkv + attention + Wo in one launch (2), attention + Wo (1), none (0)")
+    ap.add_argument("--col-kv-max", type=int, default=-1,
+                    help="XH_OPT_COL_KV_MAX: histories up to this take the column-form attention + Wo "
+                         "(-1 = library default, 0 = off)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -211,6 +214,9 @@ def main():
 
     model.set_engine(args.engine)
     model.set_option(L.OPT_FUSE_ATTN_WO, args.fuse_attn_wo)
+    if args.col_kv_max >= 0:
+        model.set_option(L.OPT_COL_KV_MAX, args.col_kv_max)
+    col_max = model.get_option(L.OPT_COL_KV_MAX) if model.engine == 0 else 0
     engine = model.engine
     prompt = prompt_tokens(c.vocab_size)
     st = InferenceState(c)
@@ -240,11 +246,18 @@ def main():
 
     # graph engine's kernels, each timed on its own (HIP events on the context stream)
     kv_len_now = min(c.max_seq_len, pos + args.steps)
-    k_us = model.time_kernel(0, args.kernel_iters)
-    k_bytes = model.kernel_bytes(0, kv_len_now)
+    # every timed step in the column form (history <= col_max): its W1/W3 launch sums the
+    # per-head Wo partials in the rmsnorm prologue (which 7), else the plain one (which 0)
+    col_all = col_max > 0 and kv_len_now <= col_max
+    w13_which = 7 if col_all else 0
+    k_us = model.time_kernel(w13_which, args.kernel_iters)
+    k_bytes = model.kernel_bytes(w13_which, kv_len_now)
     k_gbps = k_bytes / (k_us * 1e-6) / 1e9
     extra_kernels = {"gemv_w13": {"avg_us": round(k_us, 2), "GBps": round(k_gbps, 1)}}
-    for which, name in ((1, "gemv_qkv"), (2, "gemv_wo"), (3, "gemv_w2"), (4, "gemv_lm_head"), (5, "attention")):
+    timed = [(1, "gemv_qkv"), (2, "gemv_wo"), (3, "gemv_w2"), (4, "gemv_lm_head"), (5, "attention")]
+    if col_max > 0:
+        timed.append((6, "attn_wo_col"))
+    for which, name in timed:
         us = model.time_kernel(which, max(20, args.kernel_iters // 4))
         b = model.kernel_bytes(which, kv_len_now)
         extra_kernels[name] = {"avg_us": round(us, 2), "GBps": round(b / (us * 1e-6) / 1e9, 1)}
@@ -297,12 +310,14 @@ def main():
                     "bytes_per_launch": step_bytes, "avg_launch_us": round(launch_us, 1)}
     else:
         # the W1/W3 launch's exact instantiation (PF shape, see xalm_hip.hip launch_gemv_t)
-        traffic, src = pmc_traffic("void xalm::gemv_kernel<%d, 1, 3, xalm::GemvShape<512, 2, 4, true, 4, true, 2> >"
-                                   % w["wdt"])
+        traffic, src = pmc_traffic("void xalm::gemv_kernel<%d, %d, 3, xalm::GemvShape<512, 2, 4, true, 4, true, 2> >"
+                                   % (w["wdt"], 2 if col_all else 1))
         roofline = {"bound": "hbm", "achieved": round(k_gbps, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                     "frac": round(k_gbps / HBM_PEAK_GBPS, 4), "traffic": traffic,
                     "traffic_source": src,
-                    "kernel": "gemv_kernel<PRO_RMSNORM,EPI_GLU> (fused W1/W3 + rmsnorm + silu*up), layer 0",
+                    "kernel": ("gemv_kernel<PRO_RMSNORM_P,EPI_GLU> (fused W1/W3 + sum of the Wo partials + rmsnorm + "
+                               "silu*up)" if col_all else
+                               "gemv_kernel<PRO_RMSNORM,EPI_GLU> (fused W1/W3 + rmsnorm + silu*up)") + ", layer 0",
                     "bytes_per_launch": k_bytes, "avg_launch_us": round(k_us, 2)}
     value = job_value(world, args.steps, elapsed)
     if rank == 0:
@@ -323,7 +338,8 @@ def main():
                        "kv_len_timed": [pos + 1, pos + args.steps], "batch": 1, "parallelism": f"replicas x{world}",
                        "engine": "persistent" if engine == 1 else "stream (LDS-DMA weight ring)" if engine == 2 else
                        {2: "graph, qkv+attention+Wo fused", 1: "graph, attention+Wo fused",
-                        0: "graph"}[model.get_option(L.OPT_FUSE_ATTN_WO)]},
+                        0: "graph"}[model.get_option(L.OPT_FUSE_ATTN_WO)] +
+                       (f", column attention+Wo for kv_len <= {col_max}" if col_max else "")},
             "roofline": roofline,
             "hbm_step": {"achieved_GBps": round(step_gbps, 1), "frac": round(step_gbps / HBM_PEAK_GBPS, 4),
                          "bytes_per_token": step_bytes // args.steps,

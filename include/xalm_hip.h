@@ -204,7 +204,15 @@ int xh_set_graphs(xh_ctx* ctx, int enable);
  * epilogue of the W1/W3 GEMM writes those f16 hi/lo fragments directly (one launch); 0 = GLU to
  * f32 first, then split in the W2 GEMM's input pass (two launches).  Bit-identical results; a
  * debug knob so tests cover both routes. */
-enum xh_option { XH_OPT_FUSE_ATTN_WO = 1, XH_OPT_PREFILL = 2, XH_OPT_PREFILL_GLU_SPLIT = 3 };
+/* XH_OPT_COL_KV_MAX (default 0 = off, at most 256): at fusion level 1, decode steps whose
+ * history (kv_len) is at most this take the column form of attention + Wo (attn_col.h): each
+ * workgroup serves one KV head and a block of Wo rows, computes that head's attention itself and
+ * multiplies it by its slice of Wo's columns; the W1/W3 launch's rmsnorm sums the per-head
+ * partials.  No hand-off between workgroups; every workgroup of a head pulls that head's whole
+ * K/V history into LDS (served by its XCD's L2), so longer histories keep the split-KV form.  xh_get_option reports 0 where the weights or the
+ * head shape do not take it (f32 Wo beyond 64 chunks per head, exact fp8 decode, > 8 KV heads).
+ * Measured no faster than the default form on MI355X; kept as an option. */
+enum xh_option { XH_OPT_FUSE_ATTN_WO = 1, XH_OPT_PREFILL = 2, XH_OPT_PREFILL_GLU_SPLIT = 3, XH_OPT_COL_KV_MAX = 4 };
 int xh_set_option(xh_ctx* ctx, int option, int value);
 int xh_get_option(const xh_ctx* ctx, int option, int* value);
 
@@ -221,7 +229,8 @@ int xh_op_mha(float* xout, const uint16_t* kb, const uint16_t* vb, const float* 
 
 /* ---- timing hooks used by bench.py (HIP events on the context's own stream) -------- */
 /* Average device time (microseconds) of one launch of kernel `which` (0 = the fused
- * gate/up matvec of layer 0, 1 = qkv, 2 = wo, 3 = down, 4 = lm_head, 5 = attention)
+ * gate/up matvec of layer 0, 1 = qkv, 2 = wo, 3 = down, 4 = lm_head, 5 = attention, 6 = the
+ * column-form attention + Wo, 7 = the gate/up matvec summing the column form's partials)
  * over `iters` back-to-back launches with the current step parameters. */
 int xh_time_kernel(xh_ctx* ctx, int which, int iters, float* avg_us);
 /* Bytes one launch of that kernel must move (algorithmic). */

@@ -23,13 +23,16 @@ FIXTURES = ["tiny_mistral_f16", "tiny_mistral_bf16", "tiny_mistral_f32", "tiny_m
 # "graph_qaw": hipGraph of kernels per token with rmsnorm + qkv, attention and Wo in ONE launch
 # (qaw.h, the default); "graph": qkv, then attention + Wo in one launch; "graph_split": three
 # launches; "persistent": one persistent kernel per call (xh_set_engine(1))
-ENGINES = ["graph_qaw", "graph", "graph_split", "persistent"]
-FUSE = {"graph_qaw": 2, "graph": 1, "graph_split": 0, "persistent": 1}
+# "graph_col": the graph with the column-form attention + Wo (attn_col.h, XH_OPT_COL_KV_MAX)
+ENGINES = ["graph_qaw", "graph", "graph_split", "graph_col", "persistent"]
+FUSE = {"graph_qaw": 2, "graph": 1, "graph_split": 0, "graph_col": 1, "persistent": 1}
 
 
 def configure(gm, engine):
     gm.set_engine(1 if engine == "persistent" else 0)
     gm.set_option(L.OPT_FUSE_ATTN_WO, FUSE[engine])
+    if engine == "graph_col":
+        gm.set_option(L.OPT_COL_KV_MAX, 256)
     assert gm.engine == (1 if engine == "persistent" else 0)
     if engine != "persistent":
         # the level in effect: every fixture's head shape is instantiated

@@ -22,6 +22,7 @@ DTYPE_SIZE = {F32: 4, F16: 2, BF16: 2, F8_E4M3: 1, F8_E5M2: 1, U8: 1, Q8: 1}
 OPT_FUSE_ATTN_WO = 1
 OPT_PREFILL = 2
 OPT_PREFILL_GLU_SPLIT = 3
+OPT_COL_KV_MAX = 4
 
 # enum xh_tensor_kind
 EMBED, ATTN_NORM, FFN_NORM, WQ, WK, WV, WO, W1, W2, W3, FINAL_NORM, WCLS = range(12)

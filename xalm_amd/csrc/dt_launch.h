@@ -5,6 +5,7 @@
 
 #include <stddef.h>
 
+#include "attn_col.h"
 #include "attn_wo.h"
 #include "persistent.h"
 #include "qaw.h"
@@ -50,6 +51,21 @@ XALM_QAW_DECL(6)
 XALM_QAW_DECL(7)
 XALM_QAW_DECL(9)
 #undef XALM_QAW_DECL
+
+// Column-form attention + Wo for short histories (attn_col.h) for Wo dtype DT: grid =
+// n_kv_heads x row blocks.  Returns 0, or XH_E_INVALID when the shape is not instantiated or
+// a head's Wo slice is not a power-of-two number of 16-B chunks <= 64 (caller falls back).
+#define XALM_AC_DECL(DT) \
+    int acol_launch_dt##DT(const AttnArgs& aa, const AcArgs& ac, int head_dim, int qpk, hipStream_t stream);
+XALM_AC_DECL(1)
+XALM_AC_DECL(2)
+XALM_AC_DECL(3)
+XALM_AC_DECL(6)
+XALM_AC_DECL(7)
+XALM_AC_DECL(9)
+#undef XALM_AC_DECL
+// rows per wave of the column form (AcShape::RW), 0 = not instantiated for this dtype / shape
+int acol_rows_per_wave(int dt, int head_dim, int qpk);
 
 inline bool aw_instantiated(int hd, int qpk) {
     return (hd == 128 && (qpk == 4 || qpk == 8)) || (hd == 64 && qpk == 4) || (hd == 16 && qpk == 2);

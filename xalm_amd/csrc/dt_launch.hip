@@ -96,6 +96,28 @@ int qaw_go(const GemvArgs& qa, const AttnArgs& aa, const GemvArgs& wa, int n_kv_
     return hipGetLastError() == hipSuccess ? 0 : XH_E_HIP;
 }
 
+template <int DT, int HD, int QPK>
+int acol_go(const AttnArgs& aa, const AcArgs& ac, hipStream_t stream) {
+    using SH = AcShape<DT, HD, QPK>;
+    if constexpr (!SH::OK) {
+        return XH_E_INVALID;
+    } else {
+        if (ac.rows_per_wave != SH::RW) return XH_E_INVALID;
+        constexpr size_t smem = attn_wo_col_smem_bytes<HD, QPK>();
+        static_assert(smem <= 160 * 1024, "column-form LDS");
+        auto k = attn_wo_col_kernel<DT, HD, QPK>;
+        static bool attr = false;
+        if (!attr) {
+            if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
+                return XH_E_HIP;
+            attr = true;
+        }
+        const int rb = (ac.dim + SH::ROWS - 1) / SH::ROWS;
+        hipLaunchKernelGGL(k, dim3(rb * ac.n_kv_heads), dim3(AC_THREADS), smem, stream, aa, ac);
+        return hipGetLastError() == hipSuccess ? 0 : XH_E_HIP;
+    }
+}
+
 }  // namespace
 
 #define XALM_CAT2(a, b) a##b
@@ -119,6 +141,38 @@ int XALM_CAT(qaw_launch_dt, PK_DT)(const GemvArgs& qa, const AttnArgs& aa, const
     if (head_dim == 16 && qpk == 2) return qaw_go<PK_DT, 16, 2>(qa, aa, wa, n_kv_heads, t_max, n_cu, sy, stream);
     return XH_E_INVALID;
 }
+
+int XALM_CAT(acol_launch_dt, PK_DT)(const AttnArgs& aa, const AcArgs& ac, int head_dim, int qpk, hipStream_t stream) {
+    if (head_dim == 128 && qpk == 4) return acol_go<PK_DT, 128, 4>(aa, ac, stream);
+    if (head_dim == 128 && qpk == 8) return acol_go<PK_DT, 128, 8>(aa, ac, stream);
+    if (head_dim == 64 && qpk == 4) return acol_go<PK_DT, 64, 4>(aa, ac, stream);
+    if (head_dim == 16 && qpk == 2) return acol_go<PK_DT, 16, 2>(aa, ac, stream);
+    return XH_E_INVALID;
+}
+
+#if PK_DT == 2  // one definition: the shape table is dtype-generic
+namespace {
+template <int DT>
+int rw_of(int hd, int qpk) {
+    if (hd == 128 && qpk == 4) return AcShape<DT, 128, 4>::OK ? AcShape<DT, 128, 4>::RW : 0;
+    if (hd == 128 && qpk == 8) return AcShape<DT, 128, 8>::OK ? AcShape<DT, 128, 8>::RW : 0;
+    if (hd == 64 && qpk == 4) return AcShape<DT, 64, 4>::OK ? AcShape<DT, 64, 4>::RW : 0;
+    if (hd == 16 && qpk == 2) return AcShape<DT, 16, 2>::OK ? AcShape<DT, 16, 2>::RW : 0;
+    return 0;
+}
+}  // namespace
+int acol_rows_per_wave(int dt, int head_dim, int qpk) {
+    switch (dt) {
+        case XH_F32: return rw_of<XH_F32>(head_dim, qpk);
+        case XH_F16: return rw_of<XH_F16>(head_dim, qpk);
+        case XH_BF16: return rw_of<XH_BF16>(head_dim, qpk);
+        case XH_F8_E4M3: return rw_of<XH_F8_E4M3>(head_dim, qpk);
+        case XH_F8_E5M2: return rw_of<XH_F8_E5M2>(head_dim, qpk);
+        case XH_Q8: return rw_of<XH_Q8>(head_dim, qpk);
+        default: return 0;
+    }
+}
+#endif
 
 #if PK_DT != 9  // no persistent engine for Q8
 int XALM_CAT(pk_launch_dt, PK_DT)(const PkArgs& a, int dtc, int n_cu, hipStream_t stream, char* err, size_t errlen) {

@@ -140,7 +140,12 @@ struct xh_ctx {
     int ppl_cap = 0;
     int t_max_aw = 16;
     bool use_graphs = true;
-    hipGraphExec_t g_logits = nullptr, g_hydrate = nullptr, g_decode = nullptr;
+    // [0]: split-KV attention + Wo; [1]: the column form (attn_col.h) for histories <= col_kv_max
+    hipGraphExec_t g_logits[2] = {}, g_hydrate[2] = {}, g_decode[2] = {};
+    // column-form attention + Wo (attn_col.h): history bound (0 = off) and per-head partials
+    int col_kv_max = 0;
+    float* wo_part = nullptr;     // [n_kv_heads][dim]
+    unsigned* ac_err = nullptr;   // sticky device flag
     int max_gemv_waves = 4096;  // 16 waves per CU
     // persistent engine (persistent.h)
     int engine = -1;            // -1 auto, 0 graph of kernels, 1 persistent, 2 stream (stream.h)
@@ -179,6 +184,9 @@ struct xh_ctx {
 namespace {
 
 constexpr int QAW_LAYER_WORDS = (2 * CHAIN_SHARDS + 1) * CHAIN_SHARD_STRIDE;
+// XH_OPT_COL_KV_MAX default: histories up to this many slots take the column form (attn_col.h).
+// Off: measured no faster than the split-KV attention + Wo launch on MI355X
+constexpr int XH_COL_KV_MAX_DEFAULT = 0;
 unsigned* qaw_epoch(const xh_ctx* ctx) { return ctx->qaw_sync + (size_t)ctx->c.n_layers * QAW_LAYER_WORDS; }
 int* qaw_err(const xh_ctx* ctx) { return (int*)(qaw_epoch(ctx) + CHAIN_SHARD_STRIDE); }
 size_t qaw_words(const xh_config& c) { return (size_t)c.n_layers * QAW_LAYER_WORDS + 2 * CHAIN_SHARD_STRIDE; }
@@ -360,6 +368,13 @@ GemvArgs w13_args(xh_ctx* ctx, int l) {
     a.out = ctx->hb; a.act = ctx->c.act; a.sp = ctx->sp;
     return a;
 }
+// W1/W3 after the column form: x = the sum of the n_kv_heads Wo partials (head 0 holds the
+// residual), stored back to ctx->x by workgroup 0 for W2's residual add
+GemvArgs w13_col_args(xh_ctx* ctx, int l) {
+    GemvArgs a = w13_args(ctx, l);
+    a.x = ctx->wo_part; a.np = ctx->c.n_kv_heads; a.x_out = ctx->x;
+    return a;
+}
 GemvArgs w2_args(xh_ctx* ctx, int l) {
     const LayerW& w = ctx->L[l];
     GemvArgs a{};
@@ -438,6 +453,46 @@ int launch_attn_wo(xh_ctx* ctx, int l, hipStream_t s) {
     }
 }
 
+// column-form attention + Wo (attn_col.h): every layer's Wo takes it (dtype with a whole
+// power-of-two number of 16-B chunks per head slice, no exact-fp8 decode), <= AC_PMAX KV heads,
+// the graph engine with the attention + Wo fusion (level 1), a history within col_kv_max
+bool col_supported(const xh_ctx* ctx) {
+    const xh_config& c = ctx->c;
+    if (!ctx->wo_part || ctx->fuse_level != 1 || !ctx->fuse_attn_wo || c.n_kv_heads > AC_PMAX) return false;
+    if (c.dim % 4) return false;
+    for (const LayerW& w : ctx->L) {
+        if (w.wo_x) return false;
+        const int dt = w.wo_dt;
+        if (!(dt == XH_F32 || dt == XH_F16 || dt == XH_BF16 || dt == XH_F8_E4M3 || dt == XH_F8_E5M2 || dt == XH_Q8))
+            return false;
+        if (!acol_rows_per_wave(dt, c.head_dim, ctx->qpk)) return false;
+    }
+    return true;
+}
+bool use_col(const xh_ctx* ctx, int kv_len) {
+    return ctx->col_kv_max > 0 && kv_len <= std::min(ctx->col_kv_max, AC_KV_MAX) && col_supported(ctx);
+}
+int launch_attn_col(xh_ctx* ctx, int l, hipStream_t s) {
+    const LayerW& w = ctx->L[l];
+    const AttnArgs aa = attn_args(ctx, l);
+    AcArgs ac{};
+    ac.wo = w.wo; ac.row_bytes = (size_t)ctx->q_dim * dtype_size(w.wo_dt); ac.dim = ctx->c.dim;
+    ac.rows_per_wave = acol_rows_per_wave(w.wo_dt, ctx->c.head_dim, ctx->qpk);
+    ac.n_kv_heads = ctx->c.n_kv_heads; ac.x = ctx->x; ac.part = ctx->wo_part; ac.err = ctx->ac_err;
+    static const int ac_debug = getenv("XALM_AC_DEBUG") ? atoi(getenv("XALM_AC_DEBUG")) : 0;
+    ac.debug = ac_debug;
+    const int hd = ctx->c.head_dim, qpk = ctx->qpk;
+    switch (w.wo_dt) {
+        case XH_F32: return acol_launch_dt1(aa, ac, hd, qpk, s);
+        case XH_F16: return acol_launch_dt2(aa, ac, hd, qpk, s);
+        case XH_BF16: return acol_launch_dt3(aa, ac, hd, qpk, s);
+        case XH_F8_E4M3: return acol_launch_dt6(aa, ac, hd, qpk, s);
+        case XH_F8_E5M2: return acol_launch_dt7(aa, ac, hd, qpk, s);
+        case XH_Q8: return acol_launch_dt9(aa, ac, hd, qpk, s);
+        default: return XH_E_INVALID;
+    }
+}
+
 // qkv + attention + Wo launch of layer l; XH_E_INVALID = shape not instantiated (fall back)
 int launch_qaw(xh_ctx* ctx, int l, hipStream_t s) {
     const LayerW& w = ctx->L[l];
@@ -470,6 +525,11 @@ int check_aw(xh_ctx* ctx) {
         HIP_TRY(ctx, copy_sync(ctx, &e, qaw_err(ctx), sizeof(int), hipMemcpyDeviceToHost));
         if (e) return set_err(ctx, XH_E_HIP, "qkv -> attention -> Wo hand-off timed out");
     }
+    {
+        unsigned e = 0;
+        HIP_TRY(ctx, copy_sync(ctx, &e, ctx->ac_err, sizeof(unsigned), hipMemcpyDeviceToHost));
+        if (e) return set_err(ctx, XH_E_HIP, "column attention launched beyond its history bound");
+    }
     if (!ctx->fuse_attn_wo) return 0;
     std::vector<unsigned> h((size_t)ctx->c.n_layers * AW_SYNC_WORDS);
     HIP_TRY(ctx, copy_sync(ctx, h.data(), ctx->aw_sync, h.size() * sizeof(unsigned), hipMemcpyDeviceToHost));
@@ -479,7 +539,7 @@ int check_aw(xh_ctx* ctx) {
 }
 
 // greedy: the token is the argmax of the previous step's logits (argmax_embed_kernel)
-int enqueue_step(xh_ctx* ctx, hipStream_t s, bool with_logits, bool greedy = false) {
+int enqueue_step(xh_ctx* ctx, hipStream_t s, bool with_logits, bool greedy = false, bool col = false) {
     const xh_config& c = ctx->c;
     const int mb = ctx->max_gemv_waves;
     // the qaw counters expect one epoch per step that launches qaw in every layer
@@ -502,6 +562,14 @@ int enqueue_step(xh_ctx* ctx, hipStream_t s, bool with_logits, bool greedy = fal
         }
         if (!launch_gemv<PRO_RMSNORM, EPI_QKV>(kdt(w.qkv_dt, w.qkv_x), qkv_args(ctx, l), s, mb))
             return set_err(ctx, XH_E_INVALID, "layer %d: unsupported qkv dtype %d", l, w.qkv_dt);
+        if (col) {
+            // attention + Wo by columns (attn_col.h), W1/W3's rmsnorm sums the head partials
+            const int rc = launch_attn_col(ctx, l, s);
+            if (rc) return set_err(ctx, rc, "layer %d: column attention + Wo launch failed", l);
+            if (!launch_gemv<PRO_RMSNORM_P, EPI_GLU>(kdt(w.w13_dt, w.w13_x), w13_col_args(ctx, l), s, mb))
+                return set_err(ctx, XH_E_INVALID, "layer %d: unsupported w1/w3 dtype", l);
+            goto w2;
+        }
         if (use_attn_wo(ctx, l)) {
             const int rc = launch_attn_wo(ctx, l, s);
             if (rc) return set_err(ctx, rc, "layer %d: fused attention + Wo launch failed", l);
@@ -514,6 +582,7 @@ int enqueue_step(xh_ctx* ctx, hipStream_t s, bool with_logits, bool greedy = fal
     mlp:
         if (!launch_gemv<PRO_RMSNORM, EPI_GLU>(kdt(w.w13_dt, w.w13_x), w13_args(ctx, l), s, mb))
             return set_err(ctx, XH_E_INVALID, "layer %d: unsupported w1/w3 dtype", l);
+    w2:
         if (!launch_gemv<PRO_PLAIN, EPI_RESID>(kdt(w.w2_dt, w.w2_x), w2_args(ctx, l), s, mb))
             return set_err(ctx, XH_E_INVALID, "layer %d: unsupported w2 dtype", l);
     }
@@ -770,17 +839,19 @@ int run_stream(xh_ctx* ctx, const int* prompt, int n_prompt, int n_gen, int pos0
 void drop_graphs(xh_ctx* ctx) {
     ctx->pk_layers_dirty = true;
     ctx->se_layers_dirty = true;
-    if (ctx->g_logits) hipGraphExecDestroy(ctx->g_logits);
-    if (ctx->g_hydrate) hipGraphExecDestroy(ctx->g_hydrate);
-    if (ctx->g_decode) hipGraphExecDestroy(ctx->g_decode);
-    ctx->g_logits = ctx->g_hydrate = ctx->g_decode = nullptr;
+    for (int k = 0; k < 2; k++) {
+        if (ctx->g_logits[k]) hipGraphExecDestroy(ctx->g_logits[k]);
+        if (ctx->g_hydrate[k]) hipGraphExecDestroy(ctx->g_hydrate[k]);
+        if (ctx->g_decode[k]) hipGraphExecDestroy(ctx->g_decode[k]);
+        ctx->g_logits[k] = ctx->g_hydrate[k] = ctx->g_decode[k] = nullptr;
+    }
 }
 
-int capture(xh_ctx* ctx, int kind, hipGraphExec_t* out) {
+int capture(xh_ctx* ctx, int kind, bool col, hipGraphExec_t* out) {
     hipGraph_t g = nullptr;
     HIP_TRY(ctx, hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal));
     int rc = 0;
-    rc = enqueue_step(ctx, ctx->stream, kind != 1, kind == 2);
+    rc = enqueue_step(ctx, ctx->stream, kind != 1, kind == 2, col);
     hipError_t e = hipStreamEndCapture(ctx->stream, &g);
     if (rc) { if (g) hipGraphDestroy(g); return rc; }
     if (e != hipSuccess) return set_err(ctx, XH_E_HIP, "graph capture failed: %s", hipGetErrorString(e));
@@ -790,12 +861,14 @@ int capture(xh_ctx* ctx, int kind, hipGraphExec_t* out) {
     return 0;
 }
 
+// the step at host_step_params' position: the column form when its history is short enough
 int run_step(xh_ctx* ctx, bool with_logits) {
     if (with_logits) ctx->cand_valid = true;  // the lm_head launch writes candidates
-    if (!ctx->use_graphs) return enqueue_step(ctx, ctx->stream, with_logits);
-    hipGraphExec_t* ge = with_logits ? &ctx->g_logits : &ctx->g_hydrate;
+    const bool col = use_col(ctx, ctx->sp_host->kv_len);
+    if (!ctx->use_graphs) return enqueue_step(ctx, ctx->stream, with_logits, false, col);
+    hipGraphExec_t* ge = with_logits ? &ctx->g_logits[col] : &ctx->g_hydrate[col];
     if (!*ge) {
-        int rc = capture(ctx, with_logits ? 0 : 1, ge);
+        int rc = capture(ctx, with_logits ? 0 : 1, col, ge);
         if (rc) return rc;
     }
     HIP_TRY(ctx, hipGraphLaunch(*ge, ctx->stream));
@@ -1195,6 +1268,9 @@ int xh_create(const xh_config* cfg, int device_ordinal, xh_ctx** out) {
     CREATE_TRY(dmalloc(ctx, &ctx->qaw_sync, qaw_words(c)));
     CREATE_TRY(dmalloc(ctx, &ctx->cand, (size_t)ARGMAX_CANDS));
     CREATE_TRY(dmalloc(ctx, &ctx->scan_flag, (size_t)1));
+    CREATE_TRY(dmalloc(ctx, &ctx->ac_err, (size_t)1));
+    if (c.n_kv_heads <= AC_PMAX) CREATE_TRY(dmalloc(ctx, &ctx->wo_part, (size_t)c.n_kv_heads * c.dim));
+    ctx->col_kv_max = XH_COL_KV_MAX_DEFAULT;
     // fused launch: at most 16 splits per KV head (the attention workgroups stay a small part
     // of the 2-per-CU grid); partial buffers are sized for ctx->nsplit >= this
     ctx->qaw_nsplit = std::min(ctx->nsplit, 16);
@@ -1289,6 +1365,7 @@ void xh_destroy(xh_ctx* ctx) {
     hipFree(ctx->embed); hipFree(ctx->final_norm);
     hipFree(ctx->kv); hipFree(ctx->x); hipFree(ctx->q); hipFree(ctx->attn_out); hipFree(ctx->hb);
     hipFree(ctx->logits); hipFree(ctx->part_o); hipFree(ctx->part_ml); hipFree(ctx->attn_cnt); hipFree(ctx->aw_sync); hipFree(ctx->qaw_sync); hipFree(ctx->cand); hipFree(ctx->scan_flag);
+    hipFree(ctx->ac_err); hipFree(ctx->wo_part);
     hipFree(ctx->pf_tok); hipFree(ctx->pf_x); hipFree(ctx->pf_xn); hipFree(ctx->pf_q); hipFree(ctx->pf_att); hipFree(ctx->pf_h);
     hipFree(ctx->pf_xh); hipFree(ctx->pf_xl); hipFree(ctx->pf_xs);
     hipFree(ctx->pf_logits); hipFree(ctx->pf_tgt); hipFree(ctx->ppl_tgt); hipFree(ctx->ppl_prob);
@@ -1602,9 +1679,21 @@ int xh_decode_greedy(xh_ctx* ctx, int pos, int n_steps, int stop_a, int stop_b, 
     h->pos_next = pos;
     h->max_seq_len = ctx->c.max_seq_len;
     HIP_TRY(ctx, hipMemcpyAsync(&ctx->sp->step, &h->step, 3 * sizeof(int), hipMemcpyHostToDevice, ctx->stream));
-    if (ctx->use_graphs && !ctx->g_decode) {
-        rc = capture(ctx, 2, &ctx->g_decode);
-        if (rc) return rc;
+    // the step at position p has history min(p + 1, max_seq_len): the column-form graph while
+    // that is within col_kv_max
+    const int msl = ctx->c.max_seq_len;
+    auto col_at = [&](const int i) {
+        const int p = pos + i;
+        return use_col(ctx, p >= msl ? msl : p + 1);
+    };
+    if (ctx->use_graphs) {
+        for (int k = 0; k < 2; k++) {
+            const bool need = n_steps > 0 && (k ? col_at(0) : !col_at(n_steps - 1));
+            if (need && !ctx->g_decode[k]) {
+                rc = capture(ctx, 2, k == 1, &ctx->g_decode[k]);
+                if (rc) return rc;
+            }
+        }
     }
     // the first token is the argmax of the logits on the device: candidates from them if the
     // launch that produced them left none (persistent engine, or nothing yet)
@@ -1615,10 +1704,11 @@ int xh_decode_greedy(xh_ctx* ctx, int pos, int n_steps, int stop_a, int stop_b, 
     const bool stops = stop_a >= 0 || stop_b >= 0;
     int done = 0;
     for (int i = 0; i < n_steps; i++) {
+        const bool col = col_at(i);
         if (ctx->use_graphs) {
-            HIP_TRY(ctx, hipGraphLaunch(ctx->g_decode, ctx->stream));
+            HIP_TRY(ctx, hipGraphLaunch(ctx->g_decode[col], ctx->stream));
         } else {
-            rc = enqueue_step(ctx, ctx->stream, true, true);
+            rc = enqueue_step(ctx, ctx->stream, true, true, col);
             if (rc) return rc;
         }
         done = i + 1;
@@ -1823,6 +1913,7 @@ int xh_get_option(const xh_ctx* ctx, int option, int* value) {
             return 0;
         case XH_OPT_PREFILL: *value = ctx->prefill_batched ? ctx->prefill_gemm : 0; return 0;
         case XH_OPT_PREFILL_GLU_SPLIT: *value = ctx->pf_glu_split ? 1 : 0; return 0;
+        case XH_OPT_COL_KV_MAX: *value = col_supported(ctx) ? std::min(ctx->col_kv_max, AC_KV_MAX) : 0; return 0;
         default: return XH_E_INVALID;
     }
 }
@@ -1845,6 +1936,10 @@ int xh_set_option(xh_ctx* ctx, int option, int value) {
             if (value < 0 || value > 3) return set_err(ctx, XH_E_INVALID, "XH_OPT_PREFILL: 0 ... 3");
             ctx->prefill_batched = value != 0;
             if (value) ctx->prefill_gemm = value;
+            return 0;
+        case XH_OPT_COL_KV_MAX:
+            if (value < 0 || value > AC_KV_MAX) return set_err(ctx, XH_E_INVALID, "XH_OPT_COL_KV_MAX: 0 ... %d", AC_KV_MAX);
+            ctx->col_kv_max = value;
             return 0;
         case XH_OPT_PREFILL_GLU_SPLIT:
             if (value < 0 || value > 1) return set_err(ctx, XH_E_INVALID, "XH_OPT_PREFILL_GLU_SPLIT: 0 or 1");
@@ -1962,7 +2057,8 @@ int xh_op_mha(float* xout, const uint16_t* kb, const uint16_t* vb, const float* 
 // timing hooks for bench.py
 // ---------------------------------------------------------------------------------------
 int xh_time_kernel(xh_ctx* ctx, int which, int iters, float* avg_us) {
-    if (!ctx || !avg_us || iters <= 0 || which < 0 || which > 5) return XH_E_INVALID;
+    if (!ctx || !avg_us || iters <= 0 || which < 0 || which > 7) return XH_E_INVALID;
+    if (which >= 6 && !col_supported(ctx)) return set_err(ctx, XH_E_INVALID, "column form not available");
     HIP_TRY(ctx, hipSetDevice(ctx->dev));
     int rc = check_ready(ctx);
     if (rc) return rc;
@@ -1978,6 +2074,8 @@ int xh_time_kernel(xh_ctx* ctx, int which, int iters, float* avg_us) {
             case 2: return launch_gemv<PRO_PLAIN, EPI_RESID>(kdt(ctx->L[l].wo_dt, ctx->L[l].wo_x), wo_args(ctx, l), ctx->stream, mb);
             case 3: return launch_gemv<PRO_PLAIN, EPI_RESID>(kdt(ctx->L[l].w2_dt, ctx->L[l].w2_x), w2_args(ctx, l), ctx->stream, mb);
             case 4: return launch_gemv<PRO_RMSNORM, EPI_LOGITS>(kdt(ctx->wcls_dt, ctx->wcls_x), cls_args(ctx), ctx->stream, mb);
+            case 6: return launch_attn_col(ctx, l, ctx->stream) == 0;
+            case 7: return launch_gemv<PRO_RMSNORM_P, EPI_GLU>(kdt(ctx->L[l].w13_dt, ctx->L[l].w13_x), w13_col_args(ctx, l), ctx->stream, mb);
             default:
                 return launch_attn(attn_args(ctx, l), ctx->c.head_dim, ctx->qpk, ctx->c.n_kv_heads, ctx->t_max,
                                    ctx->stream);
@@ -2014,6 +2112,10 @@ size_t xh_kernel_bytes(const xh_ctx* ctx, int which, int kv_len) {
         case 3: return (size_t)c.hidden_dim * c.dim * dtype_size(w.w2_dt) + c.hidden_dim * vec + 2 * c.dim * vec;
         case 4: return (size_t)c.vocab_size * c.dim * dtype_size(ctx->wcls ? ctx->wcls_dt : ctx->embed_dt) +
                        c.dim * (vec + dtype_size(ctx->final_norm_dt)) + (size_t)c.vocab_size * vec;
+        case 6: return (size_t)ctx->q_dim * c.dim * dtype_size(w.wo_dt) + (size_t)2 * kv_len * ctx->kv_dim * 2 +
+                       (size_t)ctx->q_dim * vec + c.dim * vec + (size_t)c.n_kv_heads * c.dim * vec;
+        case 7: return (size_t)2 * c.hidden_dim * c.dim * dtype_size(w.w13_dt) + c.dim * dtype_size(w.fn_dt) +
+                       (size_t)c.n_kv_heads * c.dim * vec + c.dim * vec + (size_t)c.hidden_dim * vec;
         default: return (size_t)2 * kv_len * ctx->kv_dim * 2 + 2 * (size_t)ctx->q_dim * vec;
     }
 }
