@@ -37,7 +37,15 @@ enum xh_dtype {
     XH_F8_E4M3 = 6,
     XH_F8_E5M2 = 7,
     XH_U8 = 8,
-    XH_Q8 = 9 /* int8 * 0.01f, src/types.h:423-424 */
+    XH_Q8 = 9, /* int8 * 0.01f, src/types.h:423-424 */
+    /* The converter's gguf blocks (convert.py:176-187 `--type q8_0 / q4_0`, quants.py): 32
+     * elements per block, an f16 scale d first.  Q8_0 (quants.py:438-454): 34 B = d + 32
+     * int8, value d*q.  Q4_0 (quants.py:281-311): 18 B = d + 16 bytes, byte j holding element
+     * j (low nibble) and j+16 (high nibble), value d*(nibble-8).  Tensors are uploaded in that
+     * file layout ([rows][cols/32 blocks], header shape = bytes per row); the reference C++
+     * runtime cannot parse them (src/types.h:468-499), so the ids are this build's. */
+    XH_Q8_0 = 20,
+    XH_Q4_0 = 21
 };
 
 /* ---- tensor kinds (names as in .xalm, src/model.cpp:399-430) ----------------------- */

@@ -93,6 +93,56 @@ XS_FN uint8_t xs_to_f8(float f, int E) {
     return (uint8_t)(sign | code);
 }
 
+/* ---- gguf blocks (XH_Q8_0 / XH_Q4_0): quantize 32 floats into one block of the converter's
+ * file layout, restating quants.py (Q8_0.quantize_blocks :438-454, Q4_0.quantize_blocks
+ * :283-299) with numpy's float32 semantics: a float32 op per numpy op, float16 by RNE,
+ * np_roundf = round half away from zero, Q4_0's `trunc(float64(x) * float64(id) + 8.5)`
+ * cast to float32 (the product of two floats is exact in double, so contraction cannot
+ * change it). */
+XS_FN float xs_roundf_away(float v) {
+    const float a = fabsf(v);
+    const float fl = floorf(a);
+    const float b = fl + floorf(2.0f * (a - fl));
+    return v < 0.0f ? -b : (v > 0.0f ? b : 0.0f * v);
+}
+/* out: 34 bytes, f16 d then 32 int8 */
+XS_FN void xs_quant_q8_0(const float* v, uint8_t* out) {
+    float amax = 0.0f;
+    for (int k = 0; k < 32; k++) amax = fmaxf(amax, fabsf(v[k]));
+    const float d = amax / 127.0f;
+    const float id = d == 0.0f ? 0.0f : 1.0f / d;
+    const uint16_t dh = xs_to_f16(d);
+    out[0] = (uint8_t)(dh & 0xFFu);
+    out[1] = (uint8_t)(dh >> 8);
+    for (int k = 0; k < 32; k++) out[2 + k] = (uint8_t)(int8_t)xs_roundf_away(v[k] * id);
+}
+/* out: 18 bytes, f16 d then 16 bytes: byte j = q[j] | q[j+16] << 4 */
+XS_FN void xs_quant_q4_0(const float* v, uint8_t* out) {
+    int imax = 0;
+    float amax = fabsf(v[0]);
+    for (int k = 1; k < 32; k++)
+        if (fabsf(v[k]) > amax) { amax = fabsf(v[k]); imax = k; }  /* argmax: the first maximum */
+    const float d = v[imax] / -8.0f;
+    const float id = d == 0.0f ? 0.0f : 1.0f / d;
+    uint8_t q[32];
+    for (int k = 0; k < 32; k++) {
+        const float t = truncf((float)((double)v[k] * (double)id + 8.5));
+        q[k] = (uint8_t)(t < 0.0f ? 0.0f : (t > 15.0f ? 15.0f : t));
+    }
+    const uint16_t dh = xs_to_f16(d);
+    out[0] = (uint8_t)(dh & 0xFFu);
+    out[1] = (uint8_t)(dh >> 8);
+    for (int j = 0; j < 16; j++) out[2 + j] = (uint8_t)(q[j] | (q[j + 16] << 4));
+}
+/* synthetic block b of row r of a [rows][cols] tensor: the 32 values xs_value gives elements
+ * r*cols + 32b .. +31, quantized (dtype 20 Q8_0 / 21 Q4_0) */
+XS_FN void xs_block(uint8_t* out, int dtype, uint64_t seed, uint64_t r, uint64_t cols, uint64_t b, float mean, float std) {
+    float v[32];
+    for (int k = 0; k < 32; k++) v[k] = xs_value(seed, r * cols + 32 * b + k, mean, std);
+    if (dtype == 20) xs_quant_q8_0(v, out);
+    else xs_quant_q4_0(v, out);
+}
+
 /* dtype ids as in xalm_hip.h: 1 F32, 2 F16, 3 BF16, 6 F8_E4M3, 7 F8_E5M2 */
 XS_FN void xs_store(void* dst, uint64_t idx, int dtype, float v) {
     switch (dtype) {

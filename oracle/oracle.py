@@ -35,6 +35,8 @@ def _load():
             "xo_rope": (None, [_P, _I, _I, _I, ctypes.c_float, _I]),
             "xo_mha": (None, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I]),
             "xo_decode": (ctypes.c_float, [_I, _P, _SZ]),
+            "xo_decode_row": (ctypes.c_float, [_I, _P, _SZ, _SZ, _SZ]),
+            "xo_quantize_gq": (None, [_I, _P, _SZ, _P]),
             "xo_f32_to_f16": (ctypes.c_uint16, [ctypes.c_float]),
             "xo_f16_to_f32": (ctypes.c_float, [ctypes.c_uint16]),
             "xo_sample_argmax": (_I, [_P, _I]), "xo_sample_prob": (ctypes.c_float, [_P, _I, _I]),
@@ -103,6 +105,9 @@ class OracleModel:
         a = np.ctypeslib.as_array(fn(self.m, layer), shape=(self.c.max_seq_len, kv_dim))
         a[slot0: slot0 + rows.shape[0]] = rows
 
+    def reset(self):
+        _load().xo_reset(self.m)
+
     def active_bytes(self, pos):
         return int(_load().xo_active_bytes(self.m, pos))
 
@@ -168,6 +173,21 @@ def sample_argmax(logits):
     return int(_load().xo_sample_argmax(_p(logits), logits.size))
 
 
+def quantize_gq(dtype, values):
+    """gguf Q8_0 / Q4_0 block bytes of float32 rows (len % 32 == 0), [rows][bytes]."""
+    v = np.ascontiguousarray(values, dtype=np.float32)
+    rows = v.shape[0] if v.ndim > 1 else 1
+    nb = v.size // 32
+    out = np.empty((rows, nb // rows * GQ_BLOCK_BYTES[dtype]), dtype=np.uint8)
+    _load().xo_quantize_gq(dtype, _p(v), nb, _p(out))
+    return out
+
+
+def decode_row(dtype, data, row, n, i):
+    data = np.ascontiguousarray(data)
+    return float(_load().xo_decode_row(dtype, _p(data), row, n, i))
+
+
 def sample_prob(logits, index):
     logits = np.ascontiguousarray(logits, dtype=np.float32)
     return float(_load().xo_sample_prob(_p(logits), logits.size, index))
@@ -177,11 +197,17 @@ def num_threads():
     return int(_load().xo_num_threads())
 
 
-_NP = {1: np.float32, 2: np.uint16, 3: np.uint16, 6: np.uint8, 7: np.uint8}
+_NP = {1: np.float32, 2: np.uint16, 3: np.uint16, 6: np.uint8, 7: np.uint8, 20: np.uint8, 21: np.uint8}
+GQ_BLOCK_BYTES = {20: 34, 21: 18}  # gguf Q8_0 / Q4_0: bytes per 32-element block
 
 
 def synthetic(rows, cols, dtype, seed, mean, std):
-    """Host copy of xh_upload_synthetic's tensor (include/xalm_synth.h), dense [rows][cols]."""
+    """Host copy of xh_upload_synthetic's tensor (include/xalm_synth.h), dense [rows][cols]
+    (gguf blocks: [rows][cols/32 blocks] bytes, the converter's layout)."""
+    if dtype in GQ_BLOCK_BYTES:
+        out = np.empty((rows, cols // 32 * GQ_BLOCK_BYTES[dtype]), dtype=np.uint8)
+        _load().xo_fill_synthetic(_p(out), rows, cols, dtype, seed, mean, std)
+        return out
     out = np.empty((rows, cols) if rows > 1 else (cols,), dtype=_NP[dtype])
     _load().xo_fill_synthetic(_p(out), rows, cols, dtype, seed, mean, std)
     return out

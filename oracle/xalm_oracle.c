@@ -30,6 +30,13 @@
 void xo_fill_synthetic(void* dst, size_t rows, size_t cols, int dtype, uint64_t seed, float mean, float std) {
     const size_t n = rows * cols;
     size_t i;
+    if (dtype == XH_Q8_0 || dtype == XH_Q4_0) {
+        /* gguf blocks in the converter's file layout: [rows][cols/32 blocks] */
+        const size_t nb = cols / 32, bs = dtype == XH_Q8_0 ? 34 : 18;
+#pragma omp parallel for schedule(static)
+        for (i = 0; i < rows * nb; i++) xs_block((uint8_t*)dst + i * bs, dtype, seed, i / nb, cols, i % nb, mean, std);
+        return;
+    }
 #pragma omp parallel for schedule(static)
     for (i = 0; i < n; i++) xs_store(dst, i, dtype, xs_value(seed, i, mean, std));
 }
@@ -114,6 +121,33 @@ float xo_decode(int dtype, const void* data, size_t idx) {
     }
 }
 
+/* gguf blocks, quants.py dequantize_blocks: Q8_0 (:448-454) x * d; Q4_0 (:302-311)
+ * d * (nibble - 8), element j of a block in the low nibble of byte j (j < 16) or the high
+ * nibble of byte j - 16; d the block's leading f16.  `row` of a [rows][n] tensor in the
+ * converter's layout (n/32 blocks of 34 / 18 bytes per row). */
+static inline int xo_gq(int dtype) { return dtype == XH_Q8_0 || dtype == XH_Q4_0; }
+static inline size_t xo_gq_bs(int dtype) { return dtype == XH_Q8_0 ? 34 : 18; }
+static inline float xo_gq_elem(int dtype, const uint8_t* blk, int k) {
+    const float d = xo_f16_to_f32((uint16_t)(blk[0] | (blk[1] << 8)));
+    if (dtype == XH_Q8_0) return (float)(int8_t)blk[2 + k] * d;
+    const uint8_t b = blk[2 + (k & 15)];
+    return d * (float)((int)(k < 16 ? (b & 15u) : (b >> 4)) - 8);
+}
+float xo_decode_row(int dtype, const void* data, size_t row, size_t n, size_t i) {
+    if (!xo_gq(dtype)) return xo_decode(dtype, data, row * n + i);
+    const uint8_t* blk = (const uint8_t*)data + (row * (n / 32) + i / 32) * xo_gq_bs(dtype);
+    return xo_gq_elem(dtype, blk, (int)(i % 32));
+}
+
+/* the shared quantizer (include/xalm_synth.h, restating quants.py) over n_blocks blocks of 32
+ * floats: the converter's block bytes (tests pin it against quants.py quantize) */
+void xo_quantize_gq(int dtype, const float* v, size_t n_blocks, uint8_t* out) {
+    for (size_t b = 0; b < n_blocks; b++) {
+        if (dtype == XH_Q8_0) xs_quant_q8_0(v + 32 * b, out + 34 * b);
+        else xs_quant_q4_0(v + 32 * b, out + 18 * b);
+    }
+}
+
 static size_t dtype_bits(int dtype) {
     switch (dtype) {
         case XH_F32: return 32;
@@ -180,6 +214,18 @@ void xo_matmul(float* xout, const float* x, const void* w, const int dtype, cons
         case XH_F8_E4M3: XO_MATMUL_LOOP(uint8_t, f8e4m3_to_f32); break;
         case XH_F8_E5M2: XO_MATMUL_LOOP(uint8_t, f8e5m2_to_f32); break;
         case XH_Q8: XO_MATMUL_LOOP(int8_t, q8_to_f32); break;
+        case XH_Q8_0: case XH_Q4_0: {
+            /* dequantize (quants.py) then the reference's row loop */
+            const size_t nb = (size_t)n / 32, bs = xo_gq_bs(dtype);
+#pragma omp parallel for schedule(static)
+            for (i = 0; i < d; i++) {
+                const uint8_t* row = (const uint8_t*)w + (size_t)i * nb * bs;
+                float val = 0.0f;
+                for (int j = 0; j < n; j++) val += xo_gq_elem(dtype, row + (size_t)(j / 32) * bs, j % 32) * x[j];
+                xout[i] = val;
+            }
+            break;
+        }
         default: for (i = 0; i < d; i++) xout[i] = NAN; break;
     }
 #undef XO_MATMUL_LOOP
@@ -370,24 +416,28 @@ const float* xo_logits(const xo_model* m) { return m->logits; }
 uint16_t* xo_key_cache(xo_model* m, int layer) { return m->blocks[layer].key_cache; }
 uint16_t* xo_value_cache(xo_model* m, int layer) { return m->blocks[layer].value_cache; }
 
+/* bytes of one [n]-element row (gguf blocks: n/32 blocks) */
+static size_t row_bytes(int dtype, size_t n) { return xo_gq(dtype) ? n / 32 * xo_gq_bs(dtype) : n * dtype_bits(dtype) / 8; }
+
 /* Model::active_bytes, src/model.cpp:12-35 */
 size_t xo_active_bytes(const xo_model* m, size_t pos) {
     const xh_config* c = &m->c;
     size_t bytes = 0;
-    bytes += (size_t)c->dim * dtype_bits(m->embed.dtype) / 8;
-    bytes += (size_t)c->dim * dtype_bits(m->final_norm.dtype) / 8;
-    bytes += (size_t)c->vocab_size * c->dim * dtype_bits(m->wcls.dtype) / 8;
+    const size_t q_dim = (size_t)c->n_heads * c->head_dim, kv_dim = (size_t)c->n_kv_heads * c->head_dim;
+    bytes += row_bytes(m->embed.dtype, c->dim);
+    bytes += row_bytes(m->final_norm.dtype, c->dim);
+    bytes += (size_t)c->vocab_size * row_bytes(m->wcls.dtype, c->dim);
     for (int l = 0; l < c->n_layers; ++l) {
         const xo_tensor* t = m->blocks[l].t;
-        bytes += (size_t)c->dim * dtype_bits(t[XH_ATTN_NORM].dtype) / 8;
-        bytes += (size_t)c->dim * dtype_bits(t[XH_FFN_NORM].dtype) / 8;
-        bytes += (size_t)c->n_heads * c->head_dim * c->dim * dtype_bits(t[XH_WQ].dtype) / 8;
-        bytes += (size_t)c->n_kv_heads * c->head_dim * c->dim * dtype_bits(t[XH_WK].dtype) / 8;
-        bytes += (size_t)c->n_kv_heads * c->head_dim * c->dim * dtype_bits(t[XH_WV].dtype) / 8;
-        bytes += (size_t)c->n_heads * c->head_dim * c->dim * dtype_bits(t[XH_WO].dtype) / 8;
-        bytes += (size_t)c->dim * c->hidden_dim * dtype_bits(t[XH_W1].dtype) / 8;
-        bytes += (size_t)c->dim * c->hidden_dim * dtype_bits(t[XH_W2].dtype) / 8;
-        bytes += (size_t)c->dim * c->hidden_dim * dtype_bits(t[XH_W3].dtype) / 8;
+        bytes += row_bytes(t[XH_ATTN_NORM].dtype, c->dim);
+        bytes += row_bytes(t[XH_FFN_NORM].dtype, c->dim);
+        bytes += q_dim * row_bytes(t[XH_WQ].dtype, c->dim);
+        bytes += kv_dim * row_bytes(t[XH_WK].dtype, c->dim);
+        bytes += kv_dim * row_bytes(t[XH_WV].dtype, c->dim);
+        bytes += (size_t)c->dim * row_bytes(t[XH_WO].dtype, q_dim);
+        bytes += (size_t)c->hidden_dim * row_bytes(t[XH_W1].dtype, c->dim);
+        bytes += (size_t)c->dim * row_bytes(t[XH_W2].dtype, c->hidden_dim);
+        bytes += (size_t)c->hidden_dim * row_bytes(t[XH_W3].dtype, c->dim);
         const size_t kv_len = (size_t)c->max_seq_len < pos + 1 ? (size_t)c->max_seq_len : pos + 1;
         bytes += 2 * kv_len * c->n_kv_heads * c->head_dim * 2;
     }
@@ -396,7 +446,7 @@ size_t xo_active_bytes(const xo_model* m, size_t pos) {
 
 /* Model::_copy_embedding, src/infer.cpp:553-602 */
 static void copy_embedding(xo_model* m, const int token) {
-    for (int i = 0; i < m->c.dim; ++i) m->x[i] = xo_decode(m->embed.dtype, m->embed.data, (size_t)token * m->c.dim + i);
+    for (int i = 0; i < m->c.dim; ++i) m->x[i] = xo_decode_row(m->embed.dtype, m->embed.data, (size_t)token, m->c.dim, i);
 }
 
 /* Block::_block_cpu, src/infer.cpp:365-496 */

@@ -43,6 +43,10 @@ void xo_rope(float* vec, int d, int head_dim, int pos, float theta, int rotary_d
 void xo_mha(float* xout, float* att, const uint16_t* kb, const uint16_t* vb, const float* q,
             int head_dim, int kv_len, int max_seq_len, int n_heads, int n_kv_heads);
 float xo_decode(int dtype, const void* data, size_t idx);
+/* element i of row `row` of a [rows][n] tensor (gguf blocks: the converter's block layout) */
+float xo_decode_row(int dtype, const void* data, size_t row, size_t n, size_t i);
+/* quantize n_blocks blocks of 32 floats into gguf Q8_0 / Q4_0 block bytes (xalm_synth.h) */
+void xo_quantize_gq(int dtype, const float* v, size_t n_blocks, uint8_t* out);
 uint16_t xo_f32_to_f16(float f);
 float xo_f16_to_f32(uint16_t h);
 int xo_sample_argmax(const float* logits, int vocab);

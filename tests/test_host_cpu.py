@@ -64,7 +64,8 @@ def test_op_args_validated_before_device_use():
 
 
 @pytest.mark.parametrize("name", ["tiny_mistral_f16", "tiny_mistral_bf16", "tiny_mistral_f32",
-                                  "tiny_mistral_f8_e4m3", "tiny_mistral_f8_e5m2", "small_llama_f16"])
+                                  "tiny_mistral_f8_e4m3", "tiny_mistral_f8_e5m2", "small_llama_f16",
+                                  "tiny_mistral_q8_0", "tiny_mistral_q4_0", "small_llama_q8_0"])
 def test_xalm_reader(name):
     xf = XalmFile(fixture_path(name + ".xalm"))
     c = xf.config()
@@ -73,10 +74,18 @@ def test_xalm_reader(name):
     for layer in range(c.n_layers):
         for kind, tn in xf.layer_tensors(layer).items():
             ti = xf.tensors[tn]
-            assert ti.size == int(np.prod(ti.shape)) * L.DTYPE_SIZE[xf.dtype(tn)]
+            dt = xf.dtype(tn)
+            if dt in L.GQ_BLOCK_BYTES:
+                # gguf blocks: the header shape is [rows, bytes per row] (quants.py byte shape)
+                assert ti.size == int(np.prod(ti.shape)) and ti.shape[-1] % L.GQ_BLOCK_BYTES[dt] == 0
+            else:
+                assert ti.size == int(np.prod(ti.shape)) * L.DTYPE_SIZE[dt]
             assert ti.offset % 32 == 0  # convert.py align_offset
     # norms stay bf16 whatever the matrix type (convert.py:770-774)
     assert xf.tensors["l.0.attn.norm.weight"].type == "BF16"
+    if "q8_0" in name or "q4_0" in name:  # no boost for gguf targets (convert.py:729-744)
+        want = "Q8_0" if "q8_0" in name else "Q4_0"
+        assert xf.tensors["embed.weight"].type == want and xf.tensors["l.0.mlp.down.weight"].type == want
     if "f8_e4m3" in name:  # embed/lm_head boosted to bf16 (convert.py:729-744)
         assert xf.tensors["embed.weight"].type == "BF16"
         assert xf.tensors["l.0.attn.q.weight"].type == "F8_E4M3"

@@ -15,9 +15,17 @@ HIP_LIB_PATH = os.path.join(LIB_DIR, "libxalm_hip.so")
 
 # enum xh_dtype (the reference's Type ids, src/types.h:505-514)
 F32, F16, BF16, F8_E4M3, F8_E5M2, U8, Q8 = 1, 2, 3, 6, 7, 8, 9
+# the converter's gguf blocks (convert.py:176-187, quants.py): this build's ids
+Q8_0, Q4_0 = 20, 21
 DTYPE_BY_NAME = {"F32": F32, "F16": F16, "BF16": BF16, "F8_E4M3": F8_E4M3, "F8_E5M2": F8_E5M2,
-                 "U8": U8, "Q8": Q8}
+                 "U8": U8, "Q8": Q8, "Q8_0": Q8_0, "Q4_0": Q4_0}
 DTYPE_SIZE = {F32: 4, F16: 2, BF16: 2, F8_E4M3: 1, F8_E5M2: 1, U8: 1, Q8: 1}
+GQ_BLOCK_BYTES = {Q8_0: 34, Q4_0: 18}  # bytes per 32-element block
+
+
+def row_bytes(dtype: int, n: int) -> int:
+    """Bytes of one n-element row as uploaded (gguf blocks: n/32 blocks)."""
+    return n // 32 * GQ_BLOCK_BYTES[dtype] if dtype in GQ_BLOCK_BYTES else n * DTYPE_SIZE[dtype]
 # enum xh_option
 OPT_FUSE_ATTN_WO = 1
 OPT_PREFILL = 2

@@ -130,7 +130,6 @@ __global__ __launch_bounds__(AC_THREADS) void attn_wo_col_kernel(const AttnArgs 
 
         // ---- scores (src/infer.cpp:330-340) ----
         const float scale = 1.0f / sqrtf((float)HD);  // src/infer.cpp:338
-#pragma unroll 2
         for (int t = rr; t < t1; t += RPP) {
             float kf[8];
             WDec<XH_F16>::dec(*(const u32x4*)(kvs + (size_t)t * HD + sub * 8), kf);
@@ -168,7 +167,6 @@ __global__ __launch_bounds__(AC_THREADS) void attn_wo_col_kernel(const AttnArgs 
 #pragma unroll
             for (int i = 0; i < 8; i++) acc[h][i] = 0.f;
         const uint16_t* vs = kvs + (size_t)AC_KV_MAX * HD;
-#pragma unroll 2
         for (int t = rr; t < t1; t += RPP) {
             float vf[8];
             WDec<XH_F16>::dec(*(const u32x4*)(vs + (size_t)t * HD + sub * 8), vf);

@@ -137,6 +137,46 @@ template <> struct WDec<XH_Q8> {
     }
 };
 
+// ---- gguf blocks (XH_Q8_0, XH_Q4_0; quants.py Q8_0 :438-454, Q4_0 :281-311) --------------
+// Device rows are planar: [quant bytes][f16 scale per 32 elements], pitch a multiple of 16 B,
+// so a 16-B load is 16 int8 (Q8_0, half a block) or 32 nibbles (Q4_0, one block) and the
+// scales of a wave's chunks are one coalesced read.  WDec decodes the codes (q, q - 8); the
+// matvec multiplies each chunk's partial dot product by its block's d.
+__host__ __device__ constexpr bool gq_dt(const int dt) { return dt == XH_Q8_0 || dt == XH_Q4_0; }
+__host__ __device__ constexpr size_t gq_qbytes(const int dt, const size_t n) { return dt == XH_Q8_0 ? n : n / 2; }
+__host__ __device__ constexpr size_t gq_pitch(const int dt, const size_t n) {
+    return (gq_qbytes(dt, n) + n / 16 + 15) & ~(size_t)15;
+}
+__host__ __device__ constexpr size_t gq_block_bytes(const int dt) { return dt == XH_Q8_0 ? 34 : 18; }
+template <int DT> struct WScale { static constexpr int BLOCK = 0; };  // elements per scale (0: none)
+template <> struct WScale<XH_Q8_0> { static constexpr int BLOCK = 32; };
+template <> struct WScale<XH_Q4_0> { static constexpr int BLOCK = 32; };
+
+template <> struct WDec<XH_Q8_0> {
+    static constexpr int E = 16;
+    __device__ __forceinline__ static void dec(const u32x4 v, float* f) {
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+#pragma unroll
+            for (int k = 0; k < 4; k++) f[4 * i + k] = (float)(int8_t)((w[i] >> (8 * k)) & 0xffu);
+    }
+};
+template <> struct WDec<XH_Q4_0> {
+    static constexpr int E = 32;
+    __device__ __forceinline__ static void dec(const u32x4 v, float* f) {
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const uint32_t b = (w[i] >> (8 * k)) & 0xffu;
+                f[4 * i + k] = (float)((int)(b & 15u) - 8);        // element j = 4i + k
+                f[16 + 4 * i + k] = (float)((int)(b >> 4) - 8);    // element j + 16
+            }
+    }
+};
+
 // single-element decode (embedding gather, norm weights)
 __device__ __forceinline__ float dec1(const int dtype, const void* p, const size_t i) {
     switch (dtype) {
@@ -154,6 +194,16 @@ __device__ __forceinline__ float dec1(const int dtype, const void* p, const size
         case XH_Q8: return (1.f / 100.f) * (float)((const int8_t*)p)[i];
         default: return __builtin_nanf("");
     }
+}
+
+// element i of row `row` of a [rows][n] matrix of `dtype` (gguf blocks: the planar device rows)
+__device__ __forceinline__ float dec_row(const int dtype, const void* p, const size_t row, const int n, const int i) {
+    if (!gq_dt(dtype)) return dec1(dtype, p, row * (size_t)n + i);
+    const uint8_t* r = (const uint8_t*)p + row * gq_pitch(dtype, n);
+    const float d = (float)__builtin_bit_cast(_Float16, *(const uint16_t*)(r + gq_qbytes(dtype, n) + (i >> 5) * 2));
+    if (dtype == XH_Q8_0) return d * (float)(int8_t)r[i];
+    const uint8_t b = r[(i >> 5) * 16 + (i & 15)];
+    return d * (float)((int)((i & 16) ? (b >> 4) : (b & 15u)) - 8);
 }
 
 __device__ __forceinline__ uint16_t f32_to_f16_bits(const float f) {

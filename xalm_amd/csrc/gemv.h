@@ -347,6 +347,48 @@ __device__ __forceinline__ void gemv_chunk(const char* wrow, const size_t row_by
     gemv_compute<DT, ROWS, U>(wv, xs4, it, lane, acc);
 }
 
+// gguf blocks (WScale<DT>::BLOCK = 32): chunks [it, it+U) as gemv_chunk, and each chunk's f16
+// block scale d from the planar row tail (qbytes = quant bytes per row); a chunk's partial dot
+// product is scaled once: acc += d * sum(q * x)  (quants.py dequantizes d*q per element; the
+// same sum up to f32 reassociation)
+template <int DT, int ROWS, int U, bool NT>
+__device__ __forceinline__ void gemv_chunk_gq(const char* wrow, const size_t row_bytes, const size_t qbytes,
+                                              const float4* xs4, const int it, const int lane, float* acc) {
+    constexpr int E = WDec<DT>::E;
+    constexpr int QN = E / 4;
+    u32x4 wv[U][ROWS];
+    gemv_load<ROWS, U, NT>(wv, wrow, row_bytes, it);
+    float d[U][ROWS];
+    const char* rb = wrow - lane * 16 + qbytes;
+#pragma unroll
+    for (int u = 0; u < U; u++)
+#pragma unroll
+        for (int r = 0; r < ROWS; r++) {
+            const int blk = (((it + u) * 64 + lane) * E) / WScale<DT>::BLOCK;
+            d[u][r] = (float)__builtin_bit_cast(_Float16, *(const uint16_t*)(rb + (size_t)r * row_bytes + blk * 2));
+        }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        float4 xv[QN];
+#pragma unroll
+        for (int qd = 0; qd < QN; qd++) xv[qd] = xs4[((it + u) * QN + qd) * 64 + lane];
+#pragma unroll
+        for (int r = 0; r < ROWS; r++) {
+            float f[E];
+            WDec<DT>::dec(wv[u][r], f);
+            float s = 0.f;
+#pragma unroll
+            for (int qd = 0; qd < QN; qd++) {
+                s = fmaf(f[4 * qd + 0], xv[qd].x, s);
+                s = fmaf(f[4 * qd + 1], xv[qd].y, s);
+                s = fmaf(f[4 * qd + 2], xv[qd].z, s);
+                s = fmaf(f[4 * qd + 3], xv[qd].w, s);
+            }
+            acc[r] = fmaf(d[u][r], s, acc[r]);
+        }
+    }
+}
+
 // Row group `grp` of the matrix: lane pointer and row stride (0 for the duplicated last row
 // of an odd row count: rows past the end re-read the last row and are never stored).
 template <int ROWS>
@@ -379,11 +421,20 @@ __device__ __forceinline__ void gemv_group(const GemvArgs& a, const int g, const
     const int n_it = (n + 64 * E - 1) / (64 * E);
     size_t rstride;
     const char* wrow = gemv_row_ptr<ROWS>(a, g, lane, rstride);
-    for (; it + U <= n_full; it += U) gemv_chunk<DT, ROWS, U, S::NT>(wrow, rstride, xs4, it, lane, acc);
-    if (U > 2)
-        for (; it + 2 <= n_full; it += 2) gemv_chunk<DT, ROWS, 2, S::NT>(wrow, rstride, xs4, it, lane, acc);
-    for (; it < n_full; it++) gemv_chunk<DT, ROWS, 1, S::NT>(wrow, rstride, xs4, it, lane, acc);
-    if (it < n_it && (it * 64 + lane) * E < n) gemv_chunk<DT, ROWS, 1, S::NT>(wrow, rstride, xs4, it, lane, acc);
+    if constexpr (WScale<DT>::BLOCK > 0) {
+        const size_t qb = gq_qbytes(DT, (size_t)n);
+        for (; it + U <= n_full; it += U) gemv_chunk_gq<DT, ROWS, U, S::NT>(wrow, rstride, qb, xs4, it, lane, acc);
+        if (U > 2)
+            for (; it + 2 <= n_full; it += 2) gemv_chunk_gq<DT, ROWS, 2, S::NT>(wrow, rstride, qb, xs4, it, lane, acc);
+        for (; it < n_full; it++) gemv_chunk_gq<DT, ROWS, 1, S::NT>(wrow, rstride, qb, xs4, it, lane, acc);
+        if (it < n_it && (it * 64 + lane) * E < n) gemv_chunk_gq<DT, ROWS, 1, S::NT>(wrow, rstride, qb, xs4, it, lane, acc);
+    } else {
+        for (; it + U <= n_full; it += U) gemv_chunk<DT, ROWS, U, S::NT>(wrow, rstride, xs4, it, lane, acc);
+        if (U > 2)
+            for (; it + 2 <= n_full; it += 2) gemv_chunk<DT, ROWS, 2, S::NT>(wrow, rstride, xs4, it, lane, acc);
+        for (; it < n_full; it++) gemv_chunk<DT, ROWS, 1, S::NT>(wrow, rstride, xs4, it, lane, acc);
+        if (it < n_it && (it * 64 + lane) * E < n) gemv_chunk<DT, ROWS, 1, S::NT>(wrow, rstride, xs4, it, lane, acc);
+    }
 #pragma unroll
     for (int r = 0; r < ROWS; r++) acc[r] = wave_sum(acc[r]);
     if (lane == 0) gemv_epilogue<EPI, ROWS, SC1>(a, g * ROWS, acc, best);
@@ -503,7 +554,7 @@ __global__ __launch_bounds__(S::THREADS, S::MINW) void gemv_kernel(const GemvArg
     if (a.trace && threadIdx.x == 0) a.trace[4 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
     unsigned long long best = 0;  // EPI_LOGITS: this wave's best candidate (lane 0)
 
-    if constexpr (S::PF) {
+    if constexpr (S::PF && WScale<DT>::BLOCK == 0) {  // gguf blocks: the staged form below
         float4 xv[S::XN], nw[S::XN];
         stage_x_issue<PRO, S>(a, xv, nw);
         // unconditional (a wave past the last group re-reads that group's chunks, unused)

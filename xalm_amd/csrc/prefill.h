@@ -551,8 +551,8 @@ __global__ __launch_bounds__(256) void prefill_rmsnorm_kernel(const float* x, in
 // x rows of the pass = embedding rows of the tokens (Model::_copy_embedding)
 __global__ __launch_bounds__(256) void prefill_embed_kernel(const int* tokens, const void* emb, int dtype, int dim,
                                                             float* x) {
-    const size_t base = (size_t)tokens[blockIdx.x] * dim;
-    for (int i = threadIdx.x; i < dim; i += 256) x[(size_t)blockIdx.x * dim + i] = dec1(dtype, emb, base + i);
+    const size_t row = (size_t)tokens[blockIdx.x];
+    for (int i = threadIdx.x; i < dim; i += 256) x[(size_t)blockIdx.x * dim + i] = dec_row(dtype, emb, row, dim, i);
 }
 
 // attention of the pass's tokens: grid (n_kv_heads, nsplit, n); token t attends to slots

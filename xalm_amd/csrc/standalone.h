@@ -35,7 +35,7 @@ __global__ void rope_kernel(float* vec, int d, int head_dim, int pos, const floa
 __global__ void embed_kernel(const void* emb, int dtype, int dim, float* x, const StepParams* sp, unsigned* epoch) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i == 0 && epoch) *epoch += 1;
-    if (i < dim) x[i] = dec1(dtype, emb, (size_t)sp->token * dim + i);
+    if (i < dim) x[i] = dec_row(dtype, emb, (size_t)sp->token, dim, i);
 }
 
 // Greedy decode step head: argmax over the lm_head workgroups' candidates (Sampler::
@@ -72,8 +72,7 @@ __global__ __launch_bounds__(1024) void argmax_embed_kernel(const unsigned long 
         tok_s = tok;
     }
     __syncthreads();
-    const size_t base = (size_t)tok_s * dim;
-    for (int i = tid; i < dim; i += 1024) x[i] = dec1(dtype, emb, base + i);
+    for (int i = tid; i < dim; i += 1024) x[i] = dec_row(dtype, emb, (size_t)tok_s, dim, i);
 }
 
 // Candidates from logits already on the device (the first greedy step after logits that no

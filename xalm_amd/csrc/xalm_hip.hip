@@ -33,6 +33,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/xalm_synth.h"
@@ -58,8 +59,13 @@ size_t dtype_size(int dt) {
     }
 }
 bool matrix_dtype_ok(int dt) {
-    return dt == XH_F32 || dt == XH_F16 || dt == XH_BF16 || dt == XH_F8_E4M3 || dt == XH_F8_E5M2 || dt == XH_Q8;
+    return dt == XH_F32 || dt == XH_F16 || dt == XH_BF16 || dt == XH_F8_E4M3 || dt == XH_F8_E5M2 || dt == XH_Q8 ||
+           gq_dt(dt);
 }
+// bytes of one [n]-element row: in the device layout (gguf blocks: planar, gq_pitch) and in
+// the .xalm file / host upload (gguf blocks: n/32 blocks of gq_block_bytes)
+size_t dev_row_bytes(int dt, size_t n) { return gq_dt(dt) ? gq_pitch(dt, n) : n * dtype_size(dt); }
+size_t file_row_bytes(int dt, size_t n) { return gq_dt(dt) ? n / 32 * gq_block_bytes(dt) : n * dtype_size(dt); }
 int elems_per_16b(int dt) { return 16 / (int)dtype_size(dt); }
 // the kernel's decode form for a matrix: fp8 with NaN/Inf codes -> the exact bit decoder
 int kdt(int dt, bool special) {
@@ -259,7 +265,7 @@ template <int DT, int PRO, int EPI>
 void launch_gemv_t(const GemvArgs& a, hipStream_t s, int max_waves) {
     constexpr int E = WDec<DT>::E;
     // PF needs whole first chunks (n >= 64 E U) and x in XN float4 per thread
-    const bool pf = a.n % 4 == 0 && a.n >= 64 * E * UNROLL;
+    const bool pf = !gq_dt(DT) && a.n % 4 == 0 && a.n >= 64 * E * UNROLL;
     if (pf && a.n / 4 <= 2 * 512) launch_gemv_s<DT, PRO, EPI, ShapePF2>(a, s, max_waves);
     else if constexpr (PRO == PRO_PLAIN) {
         if (pf && a.n / 4 <= 8 * 512) launch_gemv_s<DT, PRO, EPI, ShapePF8>(a, s, max_waves);
@@ -282,6 +288,8 @@ bool launch_gemv(int dt, const GemvArgs& a, hipStream_t s, int max_blocks) {
         case XH_Q8: launch_gemv_t<XH_Q8, PRO, EPI>(a, s, max_blocks); return true;
         case XH_F8_E4M3_EXACT: launch_gemv_t<XH_F8_E4M3_EXACT, PRO, EPI>(a, s, max_blocks); return true;
         case XH_F8_E5M2_EXACT: launch_gemv_t<XH_F8_E5M2_EXACT, PRO, EPI>(a, s, max_blocks); return true;
+        case XH_Q8_0: launch_gemv_t<XH_Q8_0, PRO, EPI>(a, s, max_blocks); return true;
+        case XH_Q4_0: launch_gemv_t<XH_Q4_0, PRO, EPI>(a, s, max_blocks); return true;
         default: return false;
     }
 }
@@ -343,7 +351,7 @@ int attn_nsplit(int n_kv_heads, int max_seq_len) {
 GemvArgs qkv_args(xh_ctx* ctx, int l) {
     const LayerW& w = ctx->L[l];
     GemvArgs a{};
-    a.w = w.wqkv; a.row_bytes = (size_t)ctx->c.dim * dtype_size(w.qkv_dt);
+    a.w = w.wqkv; a.row_bytes = dev_row_bytes(w.qkv_dt, ctx->c.dim);
     a.n = ctx->c.dim; a.rows = ctx->q_dim + 2 * ctx->kv_dim; a.x = ctx->x;
     a.norm_w = w.attn_norm; a.norm_dtype = w.an_dt; a.eps = ctx->c.norm_eps;
     a.q = ctx->q; a.kcache = ctx->kcache(l); a.vcache = ctx->vcache(l);
@@ -355,14 +363,14 @@ GemvArgs qkv_args(xh_ctx* ctx, int l) {
 GemvArgs wo_args(xh_ctx* ctx, int l) {
     const LayerW& w = ctx->L[l];
     GemvArgs a{};
-    a.w = w.wo; a.row_bytes = (size_t)ctx->q_dim * dtype_size(w.wo_dt);
+    a.w = w.wo; a.row_bytes = dev_row_bytes(w.wo_dt, ctx->q_dim);
     a.n = ctx->q_dim; a.rows = ctx->c.dim; a.x = ctx->attn_out; a.out = ctx->x; a.sp = ctx->sp;
     return a;
 }
 GemvArgs w13_args(xh_ctx* ctx, int l) {
     const LayerW& w = ctx->L[l];
     GemvArgs a{};
-    a.w = w.w13; a.row_bytes = (size_t)ctx->c.dim * dtype_size(w.w13_dt);
+    a.w = w.w13; a.row_bytes = dev_row_bytes(w.w13_dt, ctx->c.dim);
     a.n = ctx->c.dim; a.rows = 2 * ctx->c.hidden_dim; a.x = ctx->x;
     a.norm_w = w.ffn_norm; a.norm_dtype = w.fn_dt; a.eps = ctx->c.norm_eps;
     a.out = ctx->hb; a.act = ctx->c.act; a.sp = ctx->sp;
@@ -378,13 +386,13 @@ GemvArgs w13_col_args(xh_ctx* ctx, int l) {
 GemvArgs w2_args(xh_ctx* ctx, int l) {
     const LayerW& w = ctx->L[l];
     GemvArgs a{};
-    a.w = w.w2; a.row_bytes = (size_t)ctx->c.hidden_dim * dtype_size(w.w2_dt);
+    a.w = w.w2; a.row_bytes = dev_row_bytes(w.w2_dt, ctx->c.hidden_dim);
     a.n = ctx->c.hidden_dim; a.rows = ctx->c.dim; a.x = ctx->hb; a.out = ctx->x; a.sp = ctx->sp;
     return a;
 }
 GemvArgs cls_args(xh_ctx* ctx) {
     GemvArgs a{};
-    a.w = ctx->wcls; a.row_bytes = (size_t)ctx->c.dim * dtype_size(ctx->wcls_dt);
+    a.w = ctx->wcls; a.row_bytes = dev_row_bytes(ctx->wcls_dt, ctx->c.dim);
     a.n = ctx->c.dim; a.rows = ctx->c.vocab_size; a.x = ctx->x;
     a.norm_w = ctx->final_norm; a.norm_dtype = ctx->final_norm_dt; a.eps = ctx->c.norm_eps;
     a.out = ctx->logits; a.sp = ctx->sp; a.cand = ctx->cand;
@@ -1064,6 +1072,10 @@ bool pf_supported(const xh_ctx* ctx, int n, int pos0) {
     if (!ctx->prefill_batched || pos0 + n > c.max_seq_len) return false;
     const int hd = c.head_dim, qpk = ctx->qpk;
     if (!((hd == 128 && (qpk == 4 || qpk == 8)) || (hd == 64 && qpk == 4) || (hd == 16 && qpk == 2))) return false;
+    // no GEMM form for the gguf blocks: those models take the token loop
+    if (gq_dt(ctx->wcls_dt)) return false;
+    for (const LayerW& w : ctx->L)
+        if (gq_dt(w.qkv_dt) || gq_dt(w.wo_dt) || gq_dt(w.w13_dt) || gq_dt(w.w2_dt)) return false;
     return c.dim % 32 == 0 && c.hidden_dim % 32 == 0 && ctx->q_dim % 32 == 0;
 }
 
@@ -1157,7 +1169,7 @@ int prefill_batched(xh_ctx* ctx, const int* tokens, int n, int pos0, int want_lo
                                         ctx->stream));
             hipLaunchKernelGGL(prefill_rmsnorm_kernel, dim3(m), dim3(256), 0, ctx->stream, (const float*)ctx->pf_x, c.dim,
                                (const void*)ctx->final_norm, ctx->final_norm_dt, c.norm_eps, ctx->pf_xn);
-            const size_t cls_rb = (size_t)c.dim * dtype_size(ctx->wcls_dt);
+            const size_t cls_rb = dev_row_bytes(ctx->wcls_dt, c.dim);
             for (int r0 = 0; r0 < c.vocab_size; r0 += PF_CLS_CHUNK) {
                 const int rows = std::min(PF_CLS_CHUNK, c.vocab_size - r0);
                 const int ks = pf_gemm(ctx, kdt(ctx->wcls_dt, ctx->wcls_x), (const char*)ctx->wcls + (size_t)r0 * cls_rb,
@@ -1414,7 +1426,8 @@ int tensor_slot(xh_ctx* ctx, int kind, int layer, int dtype, Slot* out) {
     }
     if (is_norm ? !(dtype == XH_F32 || dtype == XH_BF16) : !matrix_dtype_ok(dtype))
         return set_err(ctx, XH_E_INVALID, "tensor kind %d: unsupported dtype %d", kind, dtype);
-    const size_t rb = cols * dtype_size(dtype);
+    if (gq_dt(dtype) && cols % 32) return set_err(ctx, XH_E_INVALID, "tensor kind %d: %zu columns, not whole 32-element blocks", kind, cols);
+    const size_t rb = dev_row_bytes(dtype, cols);
     out->rows = rows;
     out->cols = cols;
     out->pitch = rb;
@@ -1527,6 +1540,45 @@ __global__ void synth_fill_kernel(char* base, size_t pitch, size_t rows, size_t 
     }
 }
 
+// gguf blocks: file layout ([rows][cols/32 blocks: f16 d, codes]) -> planar device rows
+// ([codes][d per block][zero pad], pitch gq_pitch), on the host, split over threads
+void gq_repack(int dt, const uint8_t* src, size_t rows, size_t cols, uint8_t* dst) {
+    const size_t nb = cols / 32, bs = gq_block_bytes(dt), qb = bs - 2;
+    const size_t pitch = gq_pitch(dt, cols), qbytes = gq_qbytes(dt, cols);
+    auto part = [&](size_t r0, size_t r1) {
+        for (size_t r = r0; r < r1; r++) {
+            const uint8_t* in = src + r * nb * bs;
+            uint8_t* out = dst + r * pitch;
+            for (size_t b = 0; b < nb; b++) {
+                memcpy(out + b * qb, in + b * bs + 2, qb);
+                memcpy(out + qbytes + 2 * b, in + b * bs, 2);
+            }
+            memset(out + qbytes + 2 * nb, 0, pitch - qbytes - 2 * nb);
+        }
+    };
+    const size_t nt = std::min<size_t>(16, std::max<size_t>(1, rows / 256));
+    std::vector<std::thread> th;
+    for (size_t t = 1; t < nt; t++) th.emplace_back(part, rows * t / nt, rows * (t + 1) / nt);
+    part(0, rows / nt);
+    for (auto& x : th) x.join();
+}
+
+// synthetic gguf blocks: one thread per block, the values and quantizer of xalm_synth.h
+// (xs_block: the oracle's bytes exactly), written straight into the planar rows of the slot
+__global__ void synth_gq_kernel(char* base, size_t pitch, size_t rows, size_t cols, int dtype, uint64_t seed, float mean,
+                                float std) {
+    const size_t nb = cols / 32, qb = gq_block_bytes(dtype) - 2, qbytes = gq_qbytes(dtype, cols);
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < rows * nb; i += (size_t)gridDim.x * blockDim.x) {
+        const size_t r = i / nb, b = i - r * nb;
+        uint8_t blk[34];
+        xs_block(blk, dtype, seed, r, cols, b, mean, std);
+        char* row = base + r * pitch;
+        for (size_t k = 0; k < qb; k++) row[b * qb + k] = (char)blk[2 + k];
+        row[qbytes + 2 * b] = (char)blk[0];
+        row[qbytes + 2 * b + 1] = (char)blk[1];
+    }
+}
+
 // the byte count of a tensor upload against the config (load_tensor's checks,
 // src/model.cpp:62-76), before the device layout is touched
 int check_bytes(xh_ctx* ctx, int kind, int dtype, size_t bytes) {
@@ -1542,10 +1594,10 @@ int check_bytes(xh_ctx* ctx, int kind, int dtype, size_t bytes) {
         case XH_W2: rows = c.dim; cols = c.hidden_dim; break;
         default: return set_err(ctx, XH_E_INVALID, "unknown tensor kind %d", kind);
     }
-    const size_t esz = dtype_size(dtype);
-    if (esz == 0 || bytes != rows * cols * esz)
+    const size_t rb = file_row_bytes(dtype, cols);
+    if (rb == 0 || (gq_dt(dtype) && cols % 32) || bytes != rows * rb)
         return set_err(ctx, XH_E_INVALID, "tensor kind %d: %zu bytes, expected %zu ([%zu,%zu] of dtype %d)", kind,
-                       bytes, rows * cols * esz, rows, cols, dtype);
+                       bytes, rows * rb, rows, cols, dtype);
     return 0;
 }
 
@@ -1560,6 +1612,13 @@ int xh_upload(xh_ctx* ctx, int kind, int layer, int dtype, const void* host, siz
     int rc = check_bytes(ctx, kind, dtype, bytes);
     if (!rc) rc = tensor_slot(ctx, kind, layer, dtype, &s);
     if (rc) return rc;
+    if (gq_dt(dtype)) {
+        const size_t rb = dev_row_bytes(dtype, s.cols);
+        std::vector<uint8_t> tmp(s.rows * rb);
+        gq_repack(dtype, (const uint8_t*)host, s.rows, s.cols, tmp.data());
+        HIP_TRY(ctx, copy2d_sync(ctx, s.base, s.pitch, tmp.data(), rb, rb, s.rows));
+        return 0;
+    }
     HIP_TRY(ctx, copy2d_sync(ctx, s.base, s.pitch, host, s.cols * dtype_size(dtype), s.cols * dtype_size(dtype),
                                  s.rows));
     return scan_f8(ctx, kind, layer, dtype, s);
@@ -1592,7 +1651,14 @@ int xh_upload_file(xh_ctx* ctx, int kind, int layer, int dtype, const char* path
     if (map == MAP_FAILED) return set_err(ctx, XH_E_INVALID, "%s: mmap: %s", path, strerror(map_errno));
     Slot s;
     rc = tensor_slot(ctx, kind, layer, dtype, &s);
-    if (!rc) {
+    if (!rc && gq_dt(dtype)) {
+        // gguf blocks: repacked on the host from the mapping (planar device rows)
+        const size_t rb = dev_row_bytes(dtype, s.cols);
+        std::vector<uint8_t> tmp(s.rows * rb);
+        gq_repack(dtype, (const uint8_t*)map + (offset - a0), s.rows, s.cols, tmp.data());
+        const hipError_t e = copy2d_sync(ctx, s.base, s.pitch, tmp.data(), rb, rb, s.rows);
+        if (e != hipSuccess) rc = set_err(ctx, XH_E_HIP, "%s: copy to the device: %s", path, hipGetErrorString(e));
+    } else if (!rc) {
         const size_t row_bytes = s.cols * dtype_size(dtype);
         // unregistered (e.g. a mapping the driver cannot pin) the same copy runs pageable
         const bool reg = hipHostRegister(map, len, hipHostRegisterReadOnly) == hipSuccess;
@@ -1612,8 +1678,12 @@ int xh_upload_synthetic(xh_ctx* ctx, int kind, int layer, int dtype, uint64_t se
     Slot s;
     int rc = tensor_slot(ctx, kind, layer, dtype, &s);
     if (rc) return rc;
-    hipLaunchKernelGGL(synth_fill_kernel, dim3(4096), dim3(256), 0, ctx->stream, s.base, s.pitch, s.rows, s.cols, dtype,
-                       seed, mean, std);
+    if (gq_dt(dtype))
+        hipLaunchKernelGGL(synth_gq_kernel, dim3(4096), dim3(256), 0, ctx->stream, s.base, s.pitch, s.rows, s.cols, dtype,
+                           seed, mean, std);
+    else
+        hipLaunchKernelGGL(synth_fill_kernel, dim3(4096), dim3(256), 0, ctx->stream, s.base, s.pitch, s.rows, s.cols,
+                           dtype, seed, mean, std);
     HIP_TRY(ctx, hipGetLastError());
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     return scan_f8(ctx, kind, layer, dtype, s);
@@ -1775,18 +1845,18 @@ size_t xh_active_bytes(const xh_ctx* ctx, size_t pos) {
     // Model::active_bytes, src/model.cpp:12-35
     if (!ctx) return 0;
     const xh_config& c = ctx->c;
-    size_t bytes = (size_t)c.dim * dtype_size(ctx->embed_dt);
+    size_t bytes = file_row_bytes(ctx->embed_dt, c.dim);
     bytes += (size_t)c.dim * dtype_size(ctx->final_norm_dt);
     const int wdt = ctx->wcls ? ctx->wcls_dt : ctx->embed_dt;
-    bytes += (size_t)c.vocab_size * c.dim * dtype_size(wdt);
+    bytes += (size_t)c.vocab_size * file_row_bytes(wdt, c.dim);
     const size_t kv_len = (size_t)c.max_seq_len < pos + 1 ? (size_t)c.max_seq_len : pos + 1;
     for (int l = 0; l < c.n_layers; ++l) {
         const LayerW& w = ctx->L[l];
         bytes += (size_t)c.dim * dtype_size(w.an_dt) + (size_t)c.dim * dtype_size(w.fn_dt);
-        bytes += (size_t)(ctx->q_dim + 2 * ctx->kv_dim) * c.dim * dtype_size(w.qkv_dt);
-        bytes += (size_t)ctx->q_dim * c.dim * dtype_size(w.wo_dt);
-        bytes += (size_t)2 * c.hidden_dim * c.dim * dtype_size(w.w13_dt);
-        bytes += (size_t)c.hidden_dim * c.dim * dtype_size(w.w2_dt);
+        bytes += (size_t)(ctx->q_dim + 2 * ctx->kv_dim) * file_row_bytes(w.qkv_dt, c.dim);
+        bytes += (size_t)c.dim * file_row_bytes(w.wo_dt, ctx->q_dim);
+        bytes += (size_t)2 * c.hidden_dim * file_row_bytes(w.w13_dt, c.dim);
+        bytes += (size_t)c.dim * file_row_bytes(w.w2_dt, c.hidden_dim);
         bytes += 2 * kv_len * ctx->kv_dim * 2;
     }
     return bytes;
@@ -1985,11 +2055,19 @@ int xh_op_matmul(float* xout, const float* x, const void* w, int dtype, int n, i
     if (!matrix_dtype_ok(dtype)) return set_err(nullptr, XH_E_INVALID, "unsupported dtype %d", dtype);
     DevBuf bw, bx, bo;
     int rc;
-    const size_t wbytes = (size_t)n * d * dtype_size(dtype);
+    if (gq_dt(dtype) && n % 32) return set_err(nullptr, XH_E_INVALID, "bad matmul args: n %% 32");
+    // gguf blocks: w in the file layout, repacked to the planar device rows
+    std::vector<uint8_t> gq_tmp;
+    if (gq_dt(dtype)) {
+        gq_tmp.resize((size_t)d * dev_row_bytes(dtype, n));
+        gq_repack(dtype, (const uint8_t*)w, d, n, gq_tmp.data());
+        w = gq_tmp.data();
+    }
+    const size_t wbytes = (size_t)d * dev_row_bytes(dtype, n);
     if ((rc = op_alloc(bw, wbytes, w)) || (rc = op_alloc(bx, (size_t)n * 4, x)) || (rc = op_alloc(bo, (size_t)d * 4, nullptr)))
         return rc;
     GemvArgs a{};
-    a.w = bw.p; a.row_bytes = (size_t)n * dtype_size(dtype); a.n = n; a.rows = d;
+    a.w = bw.p; a.row_bytes = dev_row_bytes(dtype, n); a.n = n; a.rows = d;
     a.x = (const float*)bx.p; a.out = (float*)bo.p;
     bool special = false;
     if (dtype == XH_F8_E4M3 || dtype == XH_F8_E5M2)
@@ -2104,17 +2182,17 @@ size_t xh_kernel_bytes(const xh_ctx* ctx, int which, int kv_len) {
     const LayerW& w = ctx->L[0];
     const size_t vec = 4;
     switch (which) {
-        case 0: return (size_t)2 * c.hidden_dim * c.dim * dtype_size(w.w13_dt) + c.dim * (vec + dtype_size(w.fn_dt)) +
+        case 0: return (size_t)2 * c.hidden_dim * file_row_bytes(w.w13_dt, c.dim) + c.dim * (vec + dtype_size(w.fn_dt)) +
                        (size_t)c.hidden_dim * vec;
-        case 1: return (size_t)(ctx->q_dim + 2 * ctx->kv_dim) * c.dim * dtype_size(w.qkv_dt) +
+        case 1: return (size_t)(ctx->q_dim + 2 * ctx->kv_dim) * file_row_bytes(w.qkv_dt, c.dim) +
                        c.dim * (vec + dtype_size(w.an_dt)) + (size_t)ctx->q_dim * vec + 2 * ctx->kv_dim * 2;
-        case 2: return (size_t)ctx->q_dim * c.dim * dtype_size(w.wo_dt) + ctx->q_dim * vec + 2 * c.dim * vec;
-        case 3: return (size_t)c.hidden_dim * c.dim * dtype_size(w.w2_dt) + c.hidden_dim * vec + 2 * c.dim * vec;
-        case 4: return (size_t)c.vocab_size * c.dim * dtype_size(ctx->wcls ? ctx->wcls_dt : ctx->embed_dt) +
+        case 2: return (size_t)c.dim * file_row_bytes(w.wo_dt, ctx->q_dim) + ctx->q_dim * vec + 2 * c.dim * vec;
+        case 3: return (size_t)c.dim * file_row_bytes(w.w2_dt, c.hidden_dim) + c.hidden_dim * vec + 2 * c.dim * vec;
+        case 4: return (size_t)c.vocab_size * file_row_bytes(ctx->wcls ? ctx->wcls_dt : ctx->embed_dt, c.dim) +
                        c.dim * (vec + dtype_size(ctx->final_norm_dt)) + (size_t)c.vocab_size * vec;
-        case 6: return (size_t)ctx->q_dim * c.dim * dtype_size(w.wo_dt) + (size_t)2 * kv_len * ctx->kv_dim * 2 +
+        case 6: return (size_t)c.dim * file_row_bytes(w.wo_dt, ctx->q_dim) + (size_t)2 * kv_len * ctx->kv_dim * 2 +
                        (size_t)ctx->q_dim * vec + c.dim * vec + (size_t)c.n_kv_heads * c.dim * vec;
-        case 7: return (size_t)2 * c.hidden_dim * c.dim * dtype_size(w.w13_dt) + c.dim * dtype_size(w.fn_dt) +
+        case 7: return (size_t)2 * c.hidden_dim * file_row_bytes(w.w13_dt, c.dim) + c.dim * dtype_size(w.fn_dt) +
                        (size_t)c.n_kv_heads * c.dim * vec + c.dim * vec + (size_t)c.hidden_dim * vec;
         default: return (size_t)2 * kv_len * ctx->kv_dim * 2 + 2 * (size_t)ctx->q_dim * vec;
     }

@@ -31,6 +31,9 @@ Model Model::from_xalm(const XalmFile& xalm, const int context, const Device dev
     Model m(c, ctx);
     auto load = [&](const std::string& name, int kind, int layer, std::vector<int> shape) {
         const TensorInfo& ti = xalm.tensors.at(name);
+        // gguf blocks (convert.py:176-187): the header holds the byte shape, 32 elements per block
+        if ((ti.type == XH_Q8_0 || ti.type == XH_Q4_0) && shape.size() == 2 && shape[1] % 32 == 0)
+            shape[1] = shape[1] / 32 * (ti.type == XH_Q8_0 ? 34 : 18);
         if (ti.shape != shape) {
             std::string a, b;
             for (int v : ti.shape) a += std::to_string(v) + ",";

@@ -23,6 +23,9 @@ int parse_type(const std::string& s) {
     if (u == "F8_E5M2") return XH_F8_E5M2;
     if (u == "U8") return XH_U8;
     if (u == "Q8") return XH_Q8;
+    // the converter's gguf blocks (convert.py:176-187); the reference runtime has no parser
+    if (u == "Q8_0") return XH_Q8_0;
+    if (u == "Q4_0") return XH_Q4_0;
     throw std::invalid_argument("invalid type: " + u);
 }
 

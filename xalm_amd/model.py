@@ -56,6 +56,10 @@ class Model:
 
     def _load(self, xf: XalmFile, kind: int, layer: int, name: str, expected_shape, direct: bool = True):
         ti = xf.tensors[name]
+        dt = xf.dtype(name)
+        if dt in L.GQ_BLOCK_BYTES and len(expected_shape) == 2 and expected_shape[1] % 32 == 0:
+            # gguf blocks (convert.py:176-187): the header holds the byte shape
+            expected_shape = (expected_shape[0], expected_shape[1] // 32 * L.GQ_BLOCK_BYTES[dt])
         if tuple(ti.shape) != tuple(expected_shape):  # src/model.cpp:381-392
             raise ValueError(f"shape mismatch for {name}: {ti.shape} vs {expected_shape} expected!")
         if direct:
