@@ -50,6 +50,14 @@ WORKLOADS = {
     "llama3-8b-f16": dict(desc="Llama-3-8B fp16, greedy decode, 4k context (configs[4])",
                           dim=4096, hidden=14336, layers=32, heads=32, kv_heads=8, head_dim=128, vocab=128256,
                           msl=4096, theta=5e5, wdt=L.F16, edt=L.F16, cdt=L.F16, dtype="f16", kv_prefill=0),
+    # SURVEY 8f-4 (not a BASELINE config): the converter's gguf blocks, every matrix including
+    # embed / lm_head (convert.py boost_type leaves gguf targets as they are)
+    "mistral-7b-q8_0": dict(desc="Mistral-7B gguf Q8_0 blocks (convert.py --type q8_0), greedy decode, 4k context",
+                            dim=4096, hidden=14336, layers=32, heads=32, kv_heads=8, head_dim=128, vocab=32000,
+                            msl=4096, theta=1e6, wdt=L.Q8_0, edt=L.Q8_0, cdt=L.Q8_0, dtype="q8_0", kv_prefill=0),
+    "mistral-7b-q4_0": dict(desc="Mistral-7B gguf Q4_0 blocks (convert.py --type q4_0), greedy decode, 4k context",
+                            dim=4096, hidden=14336, layers=32, heads=32, kv_heads=8, head_dim=128, vocab=32000,
+                            msl=4096, theta=1e6, wdt=L.Q4_0, edt=L.Q4_0, cdt=L.Q4_0, dtype="q4_0", kv_prefill=0),
 }
 
 
@@ -265,7 +273,9 @@ def main():
     # prompt processing, reported beside the decode metric: xh_prefill of a
     # synthetic prompt at positions 0.. (overwrites the ring rows the decode used; timed last)
     prefill = None
-    if args.prefill_tokens and not w["kv_prefill"] and args.prefill_tokens <= c.max_seq_len:
+    # the MFMA prompt path has no gguf-block GEMM (those models hydrate token by token)
+    batched_ok = w["wdt"] not in L.GQ_BLOCK_BYTES
+    if args.prefill_tokens and batched_ok and not w["kv_prefill"] and args.prefill_tokens <= c.max_seq_len:
         ptoks = prompt_tokens(c.vocab_size, n=args.prefill_tokens, seed=11)
         model.set_option(L.OPT_PREFILL, args.prefill_mode)
         model.prefill(ptoks[:64], 0, st)  # warm: buffers, code objects
