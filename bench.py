@@ -168,7 +168,15 @@ def cpu_baseline(w, c, prompt, gpu_logits0, gpu_tokens, n_decode):
         om.forward(gpu_tokens[i], pos, L.OUTPUT_LOGITS)
         pos += 1
     dt = time.time() - t0
-    return dict(value=n_decode / dt, unit="tok/s", cores=O.num_threads(), kind="port",
+    # SURVEY §8d also asks for a 1-thread run: one more teacher-forced token on one thread
+    threads = O.num_threads()
+    O.set_threads(1)
+    t1 = time.time()
+    om.forward(gpu_tokens[n_decode], pos, L.OUTPUT_LOGITS)
+    one = time.time() - t1
+    O.set_threads(threads)
+    return dict(value=n_decode / dt, unit="tok/s", cores=threads, kind="port",
+                one_thread={"value": 1.0 / one, "unit": "tok/s", "cores": 1, "sample": "1 decode token"},
                 sample=f"{n_decode} greedy decode tokens after a {len(prompt)}-token hydrate, full "
                        f"{w['desc'].split(',')[0]} shapes, same synthetic weights (wall clock, "
                        f"OpenMP oracle/xalm_oracle.c)",
@@ -306,7 +314,7 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not w["kv_prefill"]:
-        n = min(args.cpu_tokens, len(warm_tokens)) if warm_tokens else 0
+        n = min(args.cpu_tokens, len(warm_tokens) - 1) if warm_tokens else 0  # +1 token: the 1-thread sample
         if n:
             cpu = cpu_baseline(w, c, prompt, logits0, warm_tokens, n)
 

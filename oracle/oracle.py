@@ -40,7 +40,7 @@ def _load():
             "xo_f32_to_f16": (ctypes.c_uint16, [ctypes.c_float]),
             "xo_f16_to_f32": (ctypes.c_float, [ctypes.c_uint16]),
             "xo_sample_argmax": (_I, [_P, _I]), "xo_sample_prob": (ctypes.c_float, [_P, _I, _I]),
-            "xo_num_threads": (_I, []),
+            "xo_num_threads": (_I, []), "xo_set_threads": (None, [_I]),
             "xo_fill_synthetic": (None, [_P, _SZ, _SZ, _I, ctypes.c_uint64, ctypes.c_float, ctypes.c_float]),
         }
         for name, (res, args) in sig.items():
@@ -195,6 +195,10 @@ def sample_prob(logits, index):
 
 def num_threads():
     return int(_load().xo_num_threads())
+
+
+def set_threads(n):
+    _load().xo_set_threads(int(n))
 
 
 _NP = {1: np.float32, 2: np.uint16, 3: np.uint16, 6: np.uint8, 7: np.uint8, 20: np.uint8, 21: np.uint8}

@@ -329,6 +329,7 @@ float xo_sample_prob(const float* logits, const int vocab, const int index) {
 }
 
 int xo_num_threads(void) { return omp_get_max_threads(); }
+void xo_set_threads(int n) { omp_set_num_threads(n > 0 ? n : 1); }
 
 /* ------------------------------------------------------------------------------------ */
 /* model + InferenceState, src/model.h:96-284, src/model.cpp                             */

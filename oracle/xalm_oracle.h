@@ -52,6 +52,8 @@ float xo_f16_to_f32(uint16_t h);
 int xo_sample_argmax(const float* logits, int vocab);
 float xo_sample_prob(const float* logits, int vocab, int index);
 int xo_num_threads(void);
+/* OpenMP threads for the following calls (the 1-thread CPU baseline) */
+void xo_set_threads(int n);
 void xo_fill_synthetic(void* dst, size_t rows, size_t cols, int dtype, uint64_t seed, float mean, float std);
 
 #ifdef __cplusplus

@@ -31,5 +31,9 @@ step bench 600 python3 bench.py
 step bench_f8 600 python3 bench.py --workload mistral-7b-f8
 step bench_32k 600 python3 bench.py --workload mistral-7b-f16-32k --steps 64
 step bench_llama 600 python3 bench.py --workload llama3-8b-f16
-for b in bench bench_f8 bench_32k bench_llama; do tail -1 "$OUT/$b.log" > "$OUT/$b.json"; done
+# SURVEY 8f-4 block formats (not BASELINE configs; the oracle's per-element block decode makes
+# a CPU sample slow, so none)
+step bench_q8_0 600 python3 bench.py --workload mistral-7b-q8_0 --no-cpu-baseline
+step bench_q4_0 600 python3 bench.py --workload mistral-7b-q4_0 --no-cpu-baseline
+for b in bench bench_f8 bench_32k bench_llama bench_q8_0 bench_q4_0; do tail -1 "$OUT/$b.log" > "$OUT/$b.json"; done
 echo "== done"
