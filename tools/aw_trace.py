@@ -44,7 +44,7 @@ def main():
     us = lambda v: (v - t0) / 100.0  # noqa: E731
     nsplit = None
     # attention workgroups: stamp 1 = done (0 if it exited as an inactive split: then = start)
-    nsplit = max(1, min(512 // nkv, 128, (c.max_seq_len + 255) // 256))  # attn_nsplit
+    nsplit = max(1, min(256 // nkv, 128, (c.max_seq_len + 255) // 256))  # attn_nsplit (xalm_hip.hip)
     att = [i for i in used if i < nkv * nsplit]
     wo = [i for i in used if i >= nkv * nsplit]
     print(f"workgroups traced: {len(used)} (attention {len(att)}, wo {len(wo)})")

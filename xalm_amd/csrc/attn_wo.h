@@ -14,7 +14,8 @@
 //   loads, s_sleep, 2 s bound), then the workgroup merges the partials while staging its x
 //   image (out = sum_s e^{m_s-M} o_s / sum_s e^{m_s-M} l_s, as attention.h's merge) with sc1
 //   loads, and finishes the rows;
-// * the last Wo workgroup to finish zeroes sync[] for the next launch (ticket in sync[1]).
+// * the next launch on the stream (W1/W3 of the layer, GemvArgs::aw_reset) zeroes sync[] for
+//   the next use.
 // Attention workgroups are dispatched first (lowest block ids) and never wait on anything, so
 // progress does not depend on co-residency.  Fan-in: n_kv_heads * n_active arrivals.
 #pragma once
@@ -33,7 +34,7 @@ constexpr int AW_THREADS = AW_THREADS_OVERRIDE;
 template <int DT>
 using AwShape = GemvShape<AW_THREADS, 2, (WDec<DT>::E >= 16 ? 4 : 8), true, 4, true>;
 
-// sync (AW_SYNC_WORDS per layer): [0] head arrivals, [1] Wo workgroups done, [2] timeout flag
+// sync (AW_SYNC_WORDS per layer): [0] head arrivals, [1] unused, [2] timeout flag
 // (sticky, host-checked), [AW_FLAG0 + 32 k] "heads done" flag of XCD k: set by the last head
 // arrival, polled by that XCD's Wo workgroups (one polled line per XCD instead of every Wo
 // workgroup polling the counter the arrivals add to), reset with [0] by the last Wo workgroup
@@ -44,6 +45,9 @@ constexpr int AW_SYNC_WORDS = AW_FLAG0 + 8 * 32;
 // the Wo rows): the attention side merges instead (attn_block SIGNAL), so a Wo workgroup
 // reads one merged vector, not n_active partials per element.
 constexpr int AW_MAXS = 4;
+#ifndef AW_EARLY_WAVE0
+#define AW_EARLY_WAVE0 1
+#endif
 template <int HD>
 __device__ __forceinline__ bool aw_long(const AttnArgs& aa) {
     const int kv_len = aa.sp->kv_len;
@@ -214,8 +218,11 @@ __global__ __launch_bounds__(AW_THREADS) void attn_wo_kernel(const AttnArgs aa, 
                 for (int r = 0; r < S::ROWS; r++) xres[r] = g * S::ROWS + r < ga.rows ? ga.out[g * S::ROWS + r] : 0.f;
             }
         };
-        // waves 1.. request their Wo rows before the hand-off; wave 0 polls the flag first
-        const bool early = wid != 0;
+        // every wave requests its Wo rows before the hand-off, wave 0 too: its poll's sc1 loads
+        // complete behind its own row loads (vmcnt is in order), but those land (≈5 µs at
+        // full HBM rate) before the heads are done, while rows requested after the hand-off
+        // made wave 0 the launch's last wave by ≈1.5 µs
+        const bool early = AW_EARLY_WAVE0 || wid != 0;
         if (g < n_groups && early) fetch();
         wait_heads();
         if (g < n_groups && !early) fetch();
@@ -238,17 +245,13 @@ __global__ __launch_bounds__(AW_THREADS) void attn_wo_kernel(const AttnArgs aa, 
         u32x4 none[G::U][G::ROWS];
         gemv_rows<DT, EPI_RESID, G, false>(ga, g, nb * S::WAVES, lane, xs4, none);
     }
-    __syncthreads();
-    if (trace && threadIdx.x == 0) trace[8 * b + 2] = __builtin_amdgcn_s_memrealtime();
-    if (threadIdx.x == 0) {
-        const unsigned c = __hip_atomic_fetch_add(sync + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (c == (unsigned)nb - 1) {
-            __hip_atomic_store(sync, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(sync + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#pragma unroll
-            for (int k = 0; k < 8; k++) __hip_atomic_store(sync + AW_FLAG0 + 32 * k, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+    if (trace) {
+        __syncthreads();
+        if (threadIdx.x == 0) trace[8 * b + 2] = __builtin_amdgcn_s_memrealtime();
     }
+    // sync[0] and the flags are zeroed by the next launch on the stream (the W1/W3 matvec of
+    // this layer, GemvArgs::aw_reset): no returning ticket atomic at the end of every Wo
+    // workgroup (a round trip on the launch's tail)
 }
 
 // LDS bytes: the larger of the attention tiles (at AW_THREADS) and the Wo x image

@@ -72,6 +72,7 @@ struct GemvArgs {
     const StepParams* sp;
     unsigned long long* trace;  // debug (null = off): per workgroup [4] start, x staged, rows done
     unsigned long long* cand;   // EPI_LOGITS: [gridDim.x] argmax_key of the workgroup's best logit
+    unsigned* aw_reset;         // workgroup 0 zeroes words 0, 32, ..., 256 (attn_wo.h sync of the layer)
     int np;                     // PRO_RMSNORM_P: partial vectors at x (1 .. PRO_PMAX)
     float* x_out;               // PRO_RMSNORM_P: [n] the summed x (workgroup 0)
 };
@@ -312,6 +313,9 @@ __device__ __forceinline__ void gemv_load(u32x4 (&wv)[U][ROWS], const char* wrow
         }
 }
 
+__device__ __forceinline__ float fma_mix_lo(const uint32_t h2, const float x, float acc);
+__device__ __forceinline__ float fma_mix_hi(const uint32_t h2, const float x, float acc);
+
 template <int DT, int ROWS, int U>
 __device__ __forceinline__ void gemv_compute(const u32x4 (&wv)[U][ROWS], const float4* xs4, const int it,
                                              const int lane, float* acc) {
@@ -322,6 +326,24 @@ __device__ __forceinline__ void gemv_compute(const u32x4 (&wv)[U][ROWS], const f
         float4 xv[QN];
 #pragma unroll
         for (int qd = 0; qd < QN; qd++) xv[qd] = xs4[((it + u) * QN + qd) * 64 + lane];
+        if constexpr (DT == XH_F16) {
+            // f16 weights: v_fma_mix_f32 takes the f16 half directly (one op per element instead
+            // of a convert and an fma; the convert is exact, so the sums are bit-identical)
+#pragma unroll
+            for (int r = 0; r < ROWS; r++) {
+                float s = acc[r];
+                const uint32_t w4[4] = {wv[u][r].x, wv[u][r].y, wv[u][r].z, wv[u][r].w};
+#pragma unroll
+                for (int qd = 0; qd < QN; qd++) {
+                    s = fma_mix_lo(w4[2 * qd], xv[qd].x, s);
+                    s = fma_mix_hi(w4[2 * qd], xv[qd].y, s);
+                    s = fma_mix_lo(w4[2 * qd + 1], xv[qd].z, s);
+                    s = fma_mix_hi(w4[2 * qd + 1], xv[qd].w, s);
+                }
+                acc[r] = s;
+            }
+            continue;
+        }
 #pragma unroll
         for (int r = 0; r < ROWS; r++) {
             float f[E];
@@ -595,6 +617,7 @@ __global__ __launch_bounds__(S::THREADS, S::MINW) void gemv_kernel(const GemvArg
     const int wid = threadIdx.x >> 6;
     const int g = blockIdx.x * S::WAVES + wid;
     if (a.trace && threadIdx.x == 0) a.trace[4 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+    if (a.aw_reset && blockIdx.x == 0 && threadIdx.x < 9) a.aw_reset[32 * threadIdx.x] = 0u;
     unsigned long long best = 0;  // EPI_LOGITS: this wave's best candidate (lane 0)
 
     if constexpr (S::PF && WScale<DT>::BLOCK == 0) {  // gguf blocks: the staged form below

@@ -583,6 +583,12 @@ int enqueue_step(xh_ctx* ctx, hipStream_t s, bool with_logits, bool greedy = fal
         if (use_attn_wo(ctx, l)) {
             const int rc = launch_attn_wo(ctx, l, s);
             if (rc) return set_err(ctx, rc, "layer %d: fused attention + Wo launch failed", l);
+            // W1/W3 right behind it zeroes its hand-off words for the next step
+            GemvArgs a = w13_args(ctx, l);
+            a.aw_reset = ctx->aw_sync + (size_t)AW_SYNC_WORDS * l;
+            if (!launch_gemv<PRO_RMSNORM, EPI_GLU>(kdt(w.w13_dt, w.w13_x), a, s, mb))
+                return set_err(ctx, XH_E_INVALID, "layer %d: unsupported w1/w3 dtype", l);
+            goto w2;
         } else {
             if (!launch_attn(attn_args(ctx, l), c.head_dim, ctx->qpk, c.n_kv_heads, ctx->t_max, s))
                 return set_err(ctx, XH_E_INVALID, "unsupported head_dim %d / q-per-kv %d", c.head_dim, ctx->qpk);
