@@ -229,6 +229,25 @@ def test_prefill_gemm_paths_on_synthetic_weights(wdt, mode, glu):
     check_probs(gm2.token_probs(toks[:70]), om2, toks[:70])
 
 
+@pytest.mark.parametrize("wdt", [L.F16, L.BF16, L.F8_E4M3, L.F8_E5M2])
+def test_pipelined_gemv_decode(wdt):
+    # dim 4096: the qkv and W1/W3 launches take the pipelined gemv shape (gemv_rows_pipe, n a
+    # multiple of 64 E U: 2048 for 2-byte weights, 4096 for fp8) with 3 (W1/W3) and 1 (qkv) row
+    # groups per wave; token-loop logits at every position and the device greedy loop vs the oracle
+    gm, om = synthetic_pair(wdt, dim=4096, hidden=2048, n_layers=1)
+    st = InferenceState(gm.config)
+    toks = [1, 17, 300, 5, 99, 250]
+    for pos, tok in enumerate(toks):
+        gm.forward(st, tok, pos, L.OUTPUT_LOGITS)
+        om.forward(tok, pos)
+        assert np.abs(st.logits() - om.logits()).max() <= tol(om.logits()), pos
+    nxt = gm.decode_greedy(len(toks), 3)
+    gm.get_logits(st)
+    for i, t in enumerate(nxt):
+        om.forward(t, len(toks) + i)
+    assert np.abs(st.logits() - om.logits()).max() <= tol(om.logits())
+
+
 @pytest.mark.parametrize("wdt", [L.F16, L.F8_E4M3])
 def test_fused_glu_split_is_bit_identical(wdt):
     # the fused GLU -> split-f16 epilogue and the two-launch route produce the same W2 input

@@ -91,7 +91,18 @@ int main(int argc, char** argv) {
 #define VPF(NAME, MW, T, R, U) {NAME, [](const Mat& m, const GemvArgs& a) { \
         if (m.n <= 4096) launch_any<GemvShape<T, R, U, true, 4, true, 2>>(m, a, MW); \
         else launch_any<GemvShape<T, R, U, true, 4, true, 8>>(m, a, MW); }}
-    std::vector<Variant> vs = DT != XH_F16 ? std::vector<Variant>{
+#define VPP(NAME, MW, T, R, U, MINW) {NAME, [](const Mat& m, const GemvArgs& a) { \
+        if (m.n <= 4096) launch_any<GemvShape<T, R, U, true, MINW, true, 2, 2>>(m, a, MW); \
+        else launch_any<GemvShape<T, R, U, true, MINW, true, 8, 2>>(m, a, MW); }}
+    std::vector<Variant> vs = getenv("GB_PIPE") ? std::vector<Variant>{
+        VPF("t512 r2 u4 pf (product)", 4096, 512, 2, 4),
+        VPP("t512 r2 u4 pf pipe2", 4096, 512, 2, 4, 4),
+        VPP("t512 r2 u2 pf pipe2", 4096, 512, 2, 2, 4),
+        VPP("t512 r1 u4 pf pipe2", 4096, 512, 1, 4, 4),
+        VPP("t512 r2 u4 pf pipe2 w2048", 2048, 512, 2, 4, 2),
+        VPP("t256 r2 u4 pf pipe2", 4096, 256, 2, 4, 4),
+        VPP("t512 r4 u2 pf pipe2", 4096, 512, 4, 2, 4),
+    } : DT != XH_F16 ? std::vector<Variant>{
         VPF("t512 r2 u4 pf (product)", 4096, 512, 2, 4),
         VPF("t512 r4 u4 pf", 4096, 512, 4, 4),
         VPF("t512 r2 u4 pf w8192", 8192, 512, 2, 4),

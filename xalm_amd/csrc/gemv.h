@@ -35,8 +35,10 @@ enum { EPI_STORE = 0, EPI_RESID = 1, EPI_QKV = 2, EPI_GLU = 3, EPI_LOGITS = 4 };
 constexpr int LDS_HEAD_BYTES = 64;  // block-reduction scratch in front of the x image
 
 // Launch shape of one gemv instance.
-template <int THREADS_, int ROWS_, int U_, bool NT_ = true, int MINW_ = 4, bool PF_ = true, int XN_ = 0>
+template <int THREADS_, int ROWS_, int U_, bool NT_ = true, int MINW_ = 4, bool PF_ = true, int XN_ = 0, int PIPE_ = 1>
 struct GemvShape {
+    static constexpr int PIPE = PIPE_;         // 2: two register sets (gemv_rows_pipe; host-checked
+                                               // n % (64 E U) == 0, no gguf blocks)
     static constexpr int THREADS = THREADS_;   // workgroup size
     static constexpr int WAVES = THREADS_ / 64;
     static constexpr int ROWS = ROWS_;         // rows per wave and group (even for QKV / GLU)
@@ -529,6 +531,71 @@ __device__ __forceinline__ void gemv_rows(const GemvArgs& a, int g, const int to
     }
 }
 
+// PIPE 2: the wave's groups g, g + total_waves, ... as ONE stream of U-chunk steps (n has whole
+// steps only).  Each step's chunks go into one of two register sets, and the NEXT step's
+// chunks (the next group's first ones at a group end) are requested before the current set is
+// multiplied, so a wave keeps U to 2U chunks per row in flight instead of draining to zero at
+// every step, and a group's reduction and epilogue run behind the next group's loads.
+// FIRST: the first group's step 0 is already in `pre`.
+template <int DT, int EPI, class S, bool FIRST, bool SC1 = false>
+__device__ __forceinline__ void gemv_rows_pipe(const GemvArgs& a, const int g0, const int total_waves, const int lane,
+                                               const float4* xs4, const u32x4 (&pre)[S::U][S::ROWS],
+                                               unsigned long long* best = nullptr) {
+    constexpr int ROWS = S::ROWS, U = S::U;
+    constexpr int E = WDec<DT>::E;
+    const int n_groups = gemv_groups<S>(a);
+    if (g0 >= n_groups) return;
+    const int steps = a.n / (64 * E * U);
+    // step k of this wave: group g0 + (k / steps) * total_waves, chunks from (k % steps) * U
+    const int total = ((n_groups - g0 + total_waves - 1) / total_waves) * steps;
+    auto load = [&](u32x4 (&w)[U][ROWS], const int k) {
+        const int q = k / steps;
+        size_t rs;
+        const char* wrow = gemv_row_ptr<ROWS>(a, g0 + q * total_waves, lane, rs);
+        gemv_load<ROWS, U, S::NT>(w, wrow, rs, (k - q * steps) * U);
+    };
+    float acc[ROWS];
+#pragma unroll
+    for (int r = 0; r < ROWS; r++) acc[r] = 0.f;
+    // multiply step k's chunks; after a group's last step, its reduction and epilogue
+    auto step = [&](const u32x4 (&w)[U][ROWS], const int k) {
+        const int q = k / steps;
+        const int it = (k - q * steps) * U;
+        gemv_compute<DT, ROWS, U>(w, xs4, it, lane, acc);
+        if (it + U == steps * U) {
+#pragma unroll
+            for (int r = 0; r < ROWS; r++) acc[r] = wave_sum(acc[r]);
+            if (lane == 0) gemv_epilogue<EPI, ROWS, SC1>(a, (g0 + q * total_waves) * ROWS, acc, best);
+#pragma unroll
+            for (int r = 0; r < ROWS; r++) acc[r] = 0.f;
+        }
+    };
+    u32x4 wa[U][ROWS], wb[U][ROWS];
+    if constexpr (FIRST) {
+#pragma unroll
+        for (int u = 0; u < U; u++)
+#pragma unroll
+            for (int r = 0; r < ROWS; r++) wa[u][r] = pre[u][r];
+    } else {
+        load(wa, 0);
+    }
+    // the loads stay outside any branch, so the compiler's waits count only the older set
+    int k = 0;
+    for (; k + 2 < total; k += 2) {
+        load(wb, k + 1);
+        step(wa, k);
+        load(wa, k + 2);
+        step(wb, k + 1);
+    }
+    if (k + 1 < total) {
+        load(wb, k + 1);
+        step(wa, k);
+        step(wb, k + 1);
+    } else {
+        step(wa, k);
+    }
+}
+
 // PF staging, part 1: this thread's x float4s (and norm weights) into registers.  Issued
 // BEFORE the weight prefetch, so waiting for them (vmcnt counts in issue order) leaves the
 // weight chunks in flight.
@@ -632,15 +699,22 @@ __global__ __launch_bounds__(S::THREADS, S::MINW) void gemv_kernel(const GemvArg
         if (EPI == EPI_QKV && blockIdx.x == 0) rotate_sinks<S::THREADS>(a, a.sp->kv_sink);
         __syncthreads();
         if (a.trace && threadIdx.x == 0) a.trace[4 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
-        if (prefetched) gemv_rows<DT, EPI, S, true>(a, g, gridDim.x * S::WAVES, lane, xs4, pre, &best);
-        else gemv_rows<DT, EPI, S, false>(a, g, gridDim.x * S::WAVES, lane, xs4, pre, &best);
+        if constexpr (S::PIPE == 2) {
+            if (prefetched) gemv_rows_pipe<DT, EPI, S, true>(a, g, gridDim.x * S::WAVES, lane, xs4, pre, &best);
+        } else {
+            if (prefetched) gemv_rows<DT, EPI, S, true>(a, g, gridDim.x * S::WAVES, lane, xs4, pre, &best);
+            else gemv_rows<DT, EPI, S, false>(a, g, gridDim.x * S::WAVES, lane, xs4, pre, &best);
+        }
     } else {
         stage_x<E, PRO, S::THREADS>(a, xs4, red);
         if (EPI == EPI_QKV && blockIdx.x == 0) rotate_sinks<S::THREADS>(a, a.sp->kv_sink);
         __syncthreads();
         if (a.trace && threadIdx.x == 0) a.trace[4 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
         u32x4 none[S::U][S::ROWS];
-        gemv_rows<DT, EPI, S, false>(a, g, gridDim.x * S::WAVES, lane, xs4, none, &best);
+        if constexpr (S::PIPE == 2 && WScale<DT>::BLOCK == 0)
+            gemv_rows_pipe<DT, EPI, S, false>(a, g, gridDim.x * S::WAVES, lane, xs4, none, &best);
+        else
+            gemv_rows<DT, EPI, S, false>(a, g, gridDim.x * S::WAVES, lane, xs4, none, &best);
     }
     if constexpr (EPI == EPI_LOGITS) {
         // the workgroup's candidate: lane 0 of each wave holds its best

@@ -261,6 +261,12 @@ void launch_gemv_s(const GemvArgs& a, hipStream_t s, int max_waves) {
     hipLaunchKernelGGL(k, dim3(blocks), dim3(S::THREADS), smem, s, a);
 }
 
+// pipelined PF shape (gemv_rows_pipe: the next row step requested before the current one is
+// multiplied, across row groups too) for the qkv and W1/W3 launches: fp8 Mistral-7B decode
+// 568 -> 584 tok/s (their 4 KiB rows are one step per group, so a wave drained to zero at
+// every group), f16 unchanged (383 / 383); W2, Wo and lm_head unchanged either way
+using ShapePF2P = GemvShape<512, ROWS, UNROLL, true, 4, true, 2, 2>;  // n <= 4096
+
 template <int DT, int PRO, int EPI>
 void launch_gemv_t(const GemvArgs& a, hipStream_t s, int max_waves) {
     constexpr int E = WDec<DT>::E;
@@ -268,6 +274,10 @@ void launch_gemv_t(const GemvArgs& a, hipStream_t s, int max_waves) {
     // 303 tok/s, Q4_0 560 -> 506)
     // PF needs whole first chunks (n >= 64 E U) and x in XN float4 per thread
     const bool pf = !gq_dt(DT) && a.n % 4 == 0 && a.n >= 64 * E * UNROLL;
+    if constexpr ((EPI == EPI_QKV || EPI == EPI_GLU) && !gq_dt(DT)) {
+        if (pf && a.n / 4 <= 2 * 512 && a.n % (64 * E * UNROLL) == 0)
+            return launch_gemv_s<DT, PRO, EPI, ShapePF2P>(a, s, max_waves);
+    }
     if (pf && a.n / 4 <= 2 * 512) launch_gemv_s<DT, PRO, EPI, ShapePF2>(a, s, max_waves);
     else if constexpr (PRO == PRO_PLAIN) {
         if (pf && a.n / 4 <= 8 * 512) launch_gemv_s<DT, PRO, EPI, ShapePF8>(a, s, max_waves);
