@@ -6,7 +6,7 @@ CXX ?= g++
 CC ?= gcc
 ARCH ?= gfx950
 
-HIPFLAGS := -O3 --offload-arch=$(ARCH) -std=c++17 -fPIC -Wall -Wno-unused-function -Wno-unused-value -Wno-unused-result
+HIPFLAGS := -O3 --offload-arch=$(ARCH) -std=c++17 -fPIC -Wall -Wno-unused-function -Wno-unused-value -Wno-unused-result $(HIPFLAGS_EXTRA)
 HOSTFLAGS := -O2 -std=c++17 -fPIC -Wall -Wextra
 
 LIB := xalm_amd/lib

@@ -11,7 +11,8 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_DIR = os.path.join(_HERE, "lib")
-HIP_LIB_PATH = os.path.join(LIB_DIR, "libxalm_hip.so")
+# XALM_HIP_LIB: another build of the same library (launch-structure experiments, tools/)
+HIP_LIB_PATH = os.environ.get("XALM_HIP_LIB") or os.path.join(LIB_DIR, "libxalm_hip.so")
 
 # enum xh_dtype (the reference's Type ids, src/types.h:505-514)
 F32, F16, BF16, F8_E4M3, F8_E5M2, U8, Q8 = 1, 2, 3, 6, 7, 8, 9
