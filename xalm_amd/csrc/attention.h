@@ -38,6 +38,8 @@ struct AttnArgs {
     float* part_ml;          // [nsplit][n_heads][2]
     int* counters;           // [n_kv_heads], zero between launches
     const StepParams* sp;
+    const char* pf;          // attn_wo.h: bytes the idle splits read into the Infinity Cache
+    size_t pf_bytes;         //   (the next launch's first weight rows); 0 = none
 };
 
 // slots per split for this step: >= min_t, multiple of 16, nsplit * T >= kv_len
@@ -207,6 +209,11 @@ __device__ __forceinline__ void attn_block(const AttnArgs& a, const int g, const
             base += STEP;
         }
     }
+    // V round 1 is requested before the softmax (its loads do not depend on it), so the CU's
+    // memory pipe is not empty across the two barriers between the K and V passes (clamped:
+    // a split of one round re-reads its last row, unused)
+    u32x4 vn[ATTN_PREF];
+    ld_round(vn, a.vc, t0 + STEP);
     __syncthreads();
     ATTN_STAMP(3);
 
@@ -252,16 +259,17 @@ __device__ __forceinline__ void attn_block(const AttnArgs& a, const int g, const
                 if (t < t1) pv_row(v[p], t);
             }
         };
-        u32x4 rb[ATTN_PREF];
+        // round r + 1 is already in flight while round r is multiplied; round r + 2 goes into
+        // round r's registers right after
         int base = t0;
         for (;;) {
             if (base + STEP >= t1) { pv_round(vr, base); break; }
-            ld_round(rb, a.vc, base + STEP);
             pv_round(vr, base);
+            ld_round(vr, a.vc, base + 2 * STEP);
             base += STEP;
-            if (base + STEP >= t1) { pv_round(rb, base); break; }
-            ld_round(vr, a.vc, base + STEP);
-            pv_round(rb, base);
+            if (base + STEP >= t1) { pv_round(vn, base); break; }
+            pv_round(vn, base);
+            ld_round(vn, a.vc, base + 2 * STEP);
             base += STEP;
         }
     }
@@ -359,52 +367,71 @@ __device__ __forceinline__ void attn_block(const AttnArgs& a, const int g, const
     __syncthreads();
     if (!*flag) return;
     // merge: out = sum_s e^{m_s-M} o_s / sum_s e^{m_s-M} l_s   (per head)
-    float* wts = sc;  // [QPK][n_active] weights (sc is free now); den in red[h]
-    for (int h = wid; h < QPK; h += WAVES) {
-        float mv[2] = {-FLT_MAX, -FLT_MAX}, lv[2] = {0.f, 0.f};
-        int cnt = 0;
-        for (int j = lane; j < n_active; j += 64, cnt++) {  // n_active <= 128 -> at most 2 per lane
+    // The partials are split over MG thread groups (group k sums a contiguous range of splits,
+    // left to right; the group sums are added in group order).  Every thread requests its
+    // first MB partial values right behind its wave's (m, l) loads, so the (m, l) -> weights
+    // step and the partial loads share one round trip.
+    constexpr int MG = (THREADS / NO < WAVES - 1 ? THREADS / NO : WAVES - 1) > 0
+                           ? (THREADS / NO < WAVES - 1 ? THREADS / NO : WAVES - 1) : 1;
+    constexpr int MB = 16;  // partial values per thread per round trip
+    float* wts = sc;        // [QPK][n_active] weights (sc is free now)
+    float* den_s = red + MG * NO;  // [QPK]; red[k * NO + idx]: group sums
+    const int chunk = (n_active + MG - 1) / MG;
+    const int mgrp = tid / NO, midx = tid - mgrp * NO;
+    const bool mact = tid < MG * NO;
+    const int j0 = mgrp * chunk, j1 = min(n_active, j0 + chunk);
+    const float* msrc = a.part_o + (size_t)g * NO + midx;
+    const size_t mstride = (size_t)a.n_heads * HD;
+    {
+        // (m, l) of head min(wid, QPK - 1), up to 2 splits per lane (n_active <= 128);
+        // clamped indices so every load sits in one basic block with the partial loads
+        const int h = min(wid, QPK - 1);
+        float mv[2], lv[2];
+#pragma unroll
+        for (int c = 0; c < 2; c++) {
+            const int j = min(lane + 64 * c, n_active - 1);
             const float* mlp = a.part_ml + ((size_t)j * a.n_heads + g * QPK + h) * 2;
-            mv[cnt & 1] = ld_sc1(mlp);
-            lv[cnt & 1] = ld_sc1(mlp + 1);
+            mv[c] = ld_sc1(mlp);
+            lv[c] = ld_sc1(mlp + 1);
         }
-        const float M = wave_max(fmaxf(mv[0], mv[1]));
-        float den = 0.f;
-        cnt = 0;
-        for (int j = lane; j < n_active; j += 64, cnt++) {
-            const float f = expf(mv[cnt & 1] - M);
-            wts[h * n_active + j] = f;
-            den = fmaf(f, lv[cnt & 1], den);
+        float pv[MB];
+#pragma unroll
+        for (int k = 0; k < MB; k++) pv[k] = ld_sc1(msrc + (size_t)min(j0 + k, n_active - 1) * mstride);
+        const bool in0 = lane < n_active, in1 = lane + 64 < n_active;
+        const float M = wave_max(fmaxf(in0 ? mv[0] : -FLT_MAX, in1 ? mv[1] : -FLT_MAX));
+        const float f0 = expf(mv[0] - M), f1 = expf(mv[1] - M);
+        if (wid < QPK) {
+            if (in0) wts[h * n_active + lane] = f0;
+            if (in1) wts[h * n_active + lane + 64] = f1;
         }
+        float den = in0 ? f0 * lv[0] : 0.f;
+        den = in1 ? fmaf(f1, lv[1], den) : den;
         den = wave_sum(den);
-        if (lane == 0) red[h] = den;
+        if (wid < QPK && lane == 0) den_s[h] = den;
+        __syncthreads();
+        float num = 0.f;
+        if (mact) {
+            const float* w = wts + (midx / HD) * n_active;
+#pragma unroll
+            for (int k = 0; k < MB; k++)
+                if (j0 + k < j1) num = fmaf(w[j0 + k], pv[k], num);
+            for (int j = j0 + MB; j < j1; j += MB) {  // further round trips (chunk > MB)
+                float pw[MB];
+#pragma unroll
+                for (int k = 0; k < MB; k++) pw[k] = ld_sc1(msrc + (size_t)min(j + k, n_active - 1) * mstride);
+#pragma unroll
+                for (int k = 0; k < MB; k++)
+                    if (j + k < j1) num = fmaf(w[j + k], pw[k], num);
+            }
+            red[mgrp * NO + midx] = num;
+        }
     }
     __syncthreads();
     for (int idx = tid; idx < NO; idx += THREADS) {
-        const int h = idx / HD;
-        const float* w = wts + h * n_active;
-        const float* src = a.part_o + (size_t)g * NO + idx;
-        const size_t stride = (size_t)a.n_heads * HD;
-        float num = 0.f;
-        int j = 0;
-        // 16 partials per round trip (same left-to-right summation order)
-        for (; j + 16 <= n_active; j += 16) {
-            float pv[16];
+        float num = red[idx];
 #pragma unroll
-            for (int k = 0; k < 16; k++) pv[k] = ld_sc1(src + (j + k) * stride);
-#pragma unroll
-            for (int k = 0; k < 16; k++) num = fmaf(w[j + k], pv[k], num);
-        }
-        for (; j + 4 <= n_active; j += 4) {
-            const float p0 = ld_sc1(src + (j + 0) * stride), p1 = ld_sc1(src + (j + 1) * stride);
-            const float p2 = ld_sc1(src + (j + 2) * stride), p3 = ld_sc1(src + (j + 3) * stride);
-            num = fmaf(w[j], p0, num);
-            num = fmaf(w[j + 1], p1, num);
-            num = fmaf(w[j + 2], p2, num);
-            num = fmaf(w[j + 3], p3, num);
-        }
-        for (; j < n_active; j++) num = fmaf(w[j], ld_sc1(src + j * stride), num);
-        out_st(idx, num / red[h]);
+        for (int k = 1; k < MG; k++) num += red[k * NO + idx];
+        out_st(idx, num / den_s[idx / HD]);
     }
     head_done();
 }

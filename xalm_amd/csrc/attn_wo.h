@@ -59,63 +59,92 @@ __host__ __device__ constexpr size_t aw_image_bytes(const int n) {
     return (size_t)((n + 64 * E - 1) / (64 * E)) * 64 * E * sizeof(float);
 }
 
-// x image of the Wo rows = the merged attention output.  wts: LDS [n_heads][n_active] weights,
-// [n_heads] denominators, then the (m, l) pairs [n_active][n_heads][2].  The partial-o loads
-// of a thread's first float4 are issued together with the (m, l) loads (one round trip).
+// x image of the Wo rows = the merged attention output.  Up to AW_MAXS partials (attn_wo.h: longer
+// histories arrive merged, aw_long) every thread loads its float4 of each partial AND its head's
+// (m, l) pairs in one round trip and forms the weights itself (n_active expf per thread): no LDS
+// exchange and no barrier between the loads and the image.  More partials (qaw.h): wts (LDS
+// [n_heads][n_active] weights, [n_heads] denominators, then the (m, l) pairs) shared per head.
 template <int E, int HD, int THREADS = AW_THREADS>
 __device__ __forceinline__ void aw_stage_merged(const AttnArgs& aa, const int n, const int n_active, float4* xs4,
                                                 float* wts) {
-    constexpr int MAXS = AW_MAXS;  // prefetched partials per thread (registers beside the Wo rows)
+    constexpr int MAXS = AW_MAXS;
     const int tid = threadIdx.x;
     const int nh = aa.n_heads;
     const int n4 = n >> 2;
     const size_t stride = (size_t)nh * HD;  // floats per split in part_o
-    const bool pre = n_active <= MAXS && tid < n4;
-    u32x4 ov[MAXS];
-    if (pre) {
-#pragma unroll
-        for (int j = 0; j < MAXS; j++)
-            if (j < n_active) ov[j] = ld_sc1_x4(aa.part_o, (uint32_t)((j * stride + 4 * (size_t)tid) * 4));
-    }
-    float* ml = wts + nh * (n_active + 1);
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)aa.part_ml, 0, 0x7fffffff, 0x00020000);
-    for (int i = tid; i < n_active * nh; i += THREADS) {
-        ml[2 * i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, i * 8, 0, 16));  // sc1
-        ml[2 * i + 1] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, i * 8 + 4, 0, 16));
-    }
-    __syncthreads();
-    // per head: weights e^{m_s - M} and the denominator sum_s e^{m_s - M} l_s
-    for (int h = tid; h < nh; h += THREADS) {
-        float M = -FLT_MAX;
-        for (int j = 0; j < n_active; j++) M = fmaxf(M, ml[2 * (j * nh + h)]);
-        float den = 0.f;
-        for (int j = 0; j < n_active; j++) {
-            const float f = expf(ml[2 * (j * nh + h)] - M);
-            wts[h * n_active + j] = f;
-            den = fmaf(f, ml[2 * (j * nh + h) + 1], den);
+    if (n_active > MAXS) {
+        float* ml = wts + nh * (n_active + 1);
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)aa.part_ml, 0, 0x7fffffff, 0x00020000);
+        for (int i = tid; i < n_active * nh; i += THREADS) {
+            ml[2 * i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, i * 8, 0, 16));  // sc1
+            ml[2 * i + 1] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, i * 8 + 4, 0, 16));
         }
-        wts[nh * n_active + h] = den;
+        __syncthreads();
+        // per head: weights e^{m_s - M} and the denominator sum_s e^{m_s - M} l_s
+        for (int h = tid; h < nh; h += THREADS) {
+            float M = -FLT_MAX;
+            for (int j = 0; j < n_active; j++) M = fmaxf(M, ml[2 * (j * nh + h)]);
+            float den = 0.f;
+            for (int j = 0; j < n_active; j++) {
+                const float f = expf(ml[2 * (j * nh + h)] - M);
+                wts[h * n_active + j] = f;
+                den = fmaf(f, ml[2 * (j * nh + h) + 1], den);
+            }
+            wts[nh * n_active + h] = den;
+        }
+        __syncthreads();
+        for (int i = tid; i < n4; i += THREADS) {
+            const int h = (4 * i) / HD;
+            const float* w = wts + h * n_active;
+            float4 num = make_float4(0.f, 0.f, 0.f, 0.f);
+            for (int j = 0; j < n_active; j++) {
+                const u32x4 u = ld_sc1_x4(aa.part_o, (uint32_t)((j * stride + 4 * (size_t)i) * 4));
+                num.x = fmaf(w[j], bits_f32(u.x), num.x);
+                num.y = fmaf(w[j], bits_f32(u.y), num.y);
+                num.z = fmaf(w[j], bits_f32(u.z), num.z);
+                num.w = fmaf(w[j], bits_f32(u.w), num.w);
+            }
+            const float den = wts[nh * n_active + h];
+            const float4 v = make_float4(num.x / den, num.y / den, num.z / den, num.w / den);
+            const int c = i << 2;
+            const int it = c / (64 * E);
+            const int rem = c - it * 64 * E;
+            const int l = rem / E;
+            const int qd = (rem - l * E) >> 2;
+            xs4[(it * (E / 4) + qd) * 64 + l] = v;
+        }
+        return;
     }
-    __syncthreads();
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)aa.part_ml, 0, 0x7fffffff, 0x00020000);
     for (int i = tid; i < n4; i += THREADS) {
         const int h = (4 * i) / HD;
-        const float* w = wts + h * n_active;
-        float4 num = make_float4(0.f, 0.f, 0.f, 0.f);
-        auto add = [&](const float wj, const u32x4 u) {
-            num.x = fmaf(wj, bits_f32(u.x), num.x);
-            num.y = fmaf(wj, bits_f32(u.y), num.y);
-            num.z = fmaf(wj, bits_f32(u.z), num.z);
-            num.w = fmaf(wj, bits_f32(u.w), num.w);
-        };
-        if (pre && i == tid) {
+        u32x4 ov[MAXS];
+        float mv[MAXS], lv[MAXS];
 #pragma unroll
-            for (int j = 0; j < MAXS; j++)
-                if (j < n_active) add(w[j], ov[j]);
-        } else {
-            for (int j = 0; j < n_active; j++)
-                add(w[j], ld_sc1_x4(aa.part_o, (uint32_t)((j * stride + 4 * (size_t)i) * 4)));
+        for (int j = 0; j < MAXS; j++) {  // clamped: every load in one basic block
+            const int jj = j < n_active ? j : n_active - 1;
+            ov[j] = ld_sc1_x4(aa.part_o, (uint32_t)((jj * stride + 4 * (size_t)i) * 4));
+            const int mo = (jj * nh + h) * 8;
+            mv[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, mo, 0, 16));  // sc1
+            lv[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, mo + 4, 0, 16));
         }
-        const float den = wts[nh * n_active + h];
+        // out = sum_s e^{m_s-M} o_s / sum_s e^{m_s-M} l_s   (as attention.h's merge)
+        float M = -FLT_MAX;
+#pragma unroll
+        for (int j = 0; j < MAXS; j++) M = j < n_active ? fmaxf(M, mv[j]) : M;
+        float den = 0.f;
+        float4 num = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int j = 0; j < MAXS; j++) {
+            if (j < n_active) {
+                const float f = expf(mv[j] - M);
+                den = fmaf(f, lv[j], den);
+                num.x = fmaf(f, bits_f32(ov[j].x), num.x);
+                num.y = fmaf(f, bits_f32(ov[j].y), num.y);
+                num.z = fmaf(f, bits_f32(ov[j].z), num.z);
+                num.w = fmaf(f, bits_f32(ov[j].w), num.w);
+            }
+        }
         const float4 v = make_float4(num.x / den, num.y / den, num.z / den, num.w / den);
         const int c = i << 2;
         const int it = c / (64 * E);
@@ -140,6 +169,24 @@ __device__ __forceinline__ void aw_stage_out(const float* src, const int n, floa
     }
 }
 
+// An idle attention split (s >= n_active) reads its share of aa.pf (the first rows of the next
+// launch's weights) with default-policy loads, so they sit in the Infinity Cache when that
+// launch asks for them; HBM is otherwise idle behind the attention chain at short histories.
+__device__ __forceinline__ void aw_prefetch(const AttnArgs& aa, const int slot, const int nslots) {
+    constexpr size_t STEP = (size_t)16 * AW_THREADS * 8;  // 8 loads per thread per step
+    const size_t per = (aa.pf_bytes / nslots) / STEP * STEP;
+    const char* p = aa.pf + (size_t)slot * per + threadIdx.x * 16;
+    uint32_t acc = 0;
+    for (size_t o = 0; o < per; o += STEP) {
+        u32x4 v[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) v[k] = *(const u32x4*)(p + o + (size_t)k * 16 * AW_THREADS);
+#pragma unroll
+        for (int k = 0; k < 8; k++) acc ^= v[k].x ^ v[k].y ^ v[k].z ^ v[k].w;
+    }
+    asm volatile("" ::"v"(acc));
+}
+
 // trace (debug, null = off): per workgroup [8]: start, attention done | hand-off passed, end;
 // attention workgroups also [2] split known, [3] scores done, [4] p.V done, [5] partial drained
 template <int DT, int HD, int QPK>
@@ -159,6 +206,10 @@ __global__ __launch_bounds__(AW_THREADS) void attn_wo_kernel(const AttnArgs aa, 
     const unsigned target = (unsigned)(merged ? n_kv_heads : n_kv_heads * n_active);
     if (b < n_att) {
         const int g = b / aa.nsplit, s = b - g * aa.nsplit;
+        if (s >= n_active) {
+            if (aa.pf_bytes) aw_prefetch(aa, g * (aa.nsplit - n_active) + s - n_active, n_kv_heads * (aa.nsplit - n_active));
+            return;
+        }
         auto arrive = [&](unsigned* c) {
             const unsigned old = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (old + 1 == target) {
