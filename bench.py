@@ -328,7 +328,8 @@ def main():
                     "bytes_per_launch": step_bytes, "avg_launch_us": round(launch_us, 1)}
     else:
         # the W1/W3 launch's exact instantiation (PF shape, see xalm_hip.hip launch_gemv_t)
-        traffic, src = pmc_traffic("void xalm::gemv_kernel<%d, %d, 3, xalm::GemvShape<512, 2, 4, true, 4, true, 2> >"
+        # (the pipelined PF shape, PIPE = 2)
+        traffic, src = pmc_traffic("void xalm::gemv_kernel<%d, %d, 3, xalm::GemvShape<512, 2, 4, true, 4, true, 2, 2> >"
                                    % (w["wdt"], 2 if col_all else 1))
         roofline = {"bound": "hbm", "achieved": round(k_gbps, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                     "frac": round(k_gbps / HBM_PEAK_GBPS, 4), "traffic": traffic,
