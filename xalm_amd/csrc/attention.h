@@ -38,8 +38,6 @@ struct AttnArgs {
     float* part_ml;          // [nsplit][n_heads][2]
     int* counters;           // [n_kv_heads], zero between launches
     const StepParams* sp;
-    const char* pf;          // attn_wo.h: bytes the idle splits read into the Infinity Cache
-    size_t pf_bytes;         //   (the next launch's first weight rows); 0 = none
 };
 
 // slots per split for this step: >= min_t, multiple of 16, nsplit * T >= kv_len

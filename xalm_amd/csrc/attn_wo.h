@@ -169,24 +169,6 @@ __device__ __forceinline__ void aw_stage_out(const float* src, const int n, floa
     }
 }
 
-// An idle attention split (s >= n_active) reads its share of aa.pf (the first rows of the next
-// launch's weights) with default-policy loads, so they sit in the Infinity Cache when that
-// launch asks for them; HBM is otherwise idle behind the attention chain at short histories.
-__device__ __forceinline__ void aw_prefetch(const AttnArgs& aa, const int slot, const int nslots) {
-    constexpr size_t STEP = (size_t)16 * AW_THREADS * 8;  // 8 loads per thread per step
-    const size_t per = (aa.pf_bytes / nslots) / STEP * STEP;
-    const char* p = aa.pf + (size_t)slot * per + threadIdx.x * 16;
-    uint32_t acc = 0;
-    for (size_t o = 0; o < per; o += STEP) {
-        u32x4 v[8];
-#pragma unroll
-        for (int k = 0; k < 8; k++) v[k] = *(const u32x4*)(p + o + (size_t)k * 16 * AW_THREADS);
-#pragma unroll
-        for (int k = 0; k < 8; k++) acc ^= v[k].x ^ v[k].y ^ v[k].z ^ v[k].w;
-    }
-    asm volatile("" ::"v"(acc));
-}
-
 // trace (debug, null = off): per workgroup [8]: start, attention done | hand-off passed, end;
 // attention workgroups also [2] split known, [3] scores done, [4] p.V done, [5] partial drained
 template <int DT, int HD, int QPK>
@@ -206,10 +188,7 @@ __global__ __launch_bounds__(AW_THREADS) void attn_wo_kernel(const AttnArgs aa, 
     const unsigned target = (unsigned)(merged ? n_kv_heads : n_kv_heads * n_active);
     if (b < n_att) {
         const int g = b / aa.nsplit, s = b - g * aa.nsplit;
-        if (s >= n_active) {
-            if (aa.pf_bytes) aw_prefetch(aa, g * (aa.nsplit - n_active) + s - n_active, n_kv_heads * (aa.nsplit - n_active));
-            return;
-        }
+        if (s >= n_active) return;  // a split past kv_len
         auto arrive = [&](unsigned* c) {
             const unsigned old = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (old + 1 == target) {

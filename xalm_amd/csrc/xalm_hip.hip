@@ -266,10 +266,7 @@ void launch_gemv_s(const GemvArgs& a, hipStream_t s, int max_waves) {
 // 568 -> 584 tok/s (their 4 KiB rows are one step per group, so a wave drained to zero at
 // every group), f16 unchanged (383 / 383); W2, Wo and lm_head unchanged either way
 using ShapePF2P = GemvShape<512, ROWS, UNROLL, true, 4, true, 2, 2>;  // n <= 4096
-#ifndef XH_W13_NT
-#define XH_W13_NT 1
-#endif
-using ShapePF2PG = GemvShape<512, ROWS, UNROLL, XH_W13_NT, 4, true, 2, 2>;  // W1/W3
+
 
 template <int DT, int PRO, int EPI>
 void launch_gemv_t(const GemvArgs& a, hipStream_t s, int max_waves) {
@@ -279,10 +276,8 @@ void launch_gemv_t(const GemvArgs& a, hipStream_t s, int max_waves) {
     // PF needs whole first chunks (n >= 64 E U) and x in XN float4 per thread
     const bool pf = !gq_dt(DT) && a.n % 4 == 0 && a.n >= 64 * E * UNROLL;
     if constexpr ((EPI == EPI_QKV || EPI == EPI_GLU) && !gq_dt(DT)) {
-        if (pf && a.n / 4 <= 2 * 512 && a.n % (64 * E * UNROLL) == 0) {
-            if constexpr (EPI == EPI_GLU) return launch_gemv_s<DT, PRO, EPI, ShapePF2PG>(a, s, max_waves);
+        if (pf && a.n / 4 <= 2 * 512 && a.n % (64 * E * UNROLL) == 0)
             return launch_gemv_s<DT, PRO, EPI, ShapePF2P>(a, s, max_waves);
-        }
     }
     if (pf && a.n / 4 <= 2 * 512) launch_gemv_s<DT, PRO, EPI, ShapePF2>(a, s, max_waves);
     else if constexpr (PRO == PRO_PLAIN) {
@@ -463,16 +458,8 @@ bool use_attn_wo(const xh_ctx* ctx, int l) {
 }
 
 int launch_attn_wo(xh_ctx* ctx, int l, hipStream_t s) {
-    AttnArgs aa = attn_args(ctx, l);
+    const AttnArgs aa = attn_args(ctx, l);
     const GemvArgs ga = wo_args(ctx, l);
-    {
-        // XALM_AW_PF_MB: MiB of this layer's W1/W3 rows the idle attention splits pull into the
-        // Infinity Cache (experiment)
-        static const long pf_mb = getenv("XALM_AW_PF_MB") ? atol(getenv("XALM_AW_PF_MB")) : 0;
-        const size_t w13_bytes = (size_t)2 * ctx->c.hidden_dim * dev_row_bytes(ctx->L[l].w13_dt, ctx->c.dim);
-        aa.pf = (const char*)ctx->L[l].w13;
-        aa.pf_bytes = std::min((size_t)pf_mb << 20, w13_bytes);
-    }
     unsigned* sync = ctx->aw_sync + (size_t)AW_SYNC_WORDS * l;
     const int hd = ctx->c.head_dim, qpk = ctx->qpk, nkv = ctx->c.n_kv_heads, tm = ctx->t_max_aw;
     const int mw = ctx->max_gemv_waves;
