@@ -54,6 +54,13 @@ def main():
         print(f"attention start  min {a_start.min():6.2f} max {a_start.max():6.2f} us")
         if a_done.size:
             print(f"attention done   min {a_done.min():6.2f} med {np.median(a_done):6.2f} max {a_done.max():6.2f} us")
+        if a_done.size:
+            per = []
+            for g in range(nkv):
+                d = [us(t[i, 1]) for i in att if i // nsplit == g and t[i, 1]]
+                if d:
+                    per.append(f"h{g} {np.median(d):5.1f}/{max(d):5.1f}")
+            print("  done per KV head (median/max us): " + "  ".join(per))
         act = [i for i in att if t[i, 5]]
         for k, name in ((2, "split known"), (3, "scores done"), (6, "softmax done"), (7, "p.V summed"), (4, "p.V reduced"),
                         (5, "partial drained"), (1, "signalled")):

@@ -94,7 +94,19 @@ int main(int argc, char** argv) {
 #define VPP(NAME, MW, T, R, U, MINW) {NAME, [](const Mat& m, const GemvArgs& a) { \
         if (m.n <= 4096) launch_any<GemvShape<T, R, U, true, MINW, true, 2, 2>>(m, a, MW); \
         else launch_any<GemvShape<T, R, U, true, MINW, true, 8, 2>>(m, a, MW); }}
-    std::vector<Variant> vs = getenv("GB_PIPE") ? std::vector<Variant>{
+    // 1024-thread workgroups (one per CU: a CU's second workgroup no longer stages x behind the
+    // first one's weight requests); x in 1 float4 per thread for n <= 4096, else 4
+#define VPK(NAME, MW, R, U) {NAME, [](const Mat& m, const GemvArgs& a) { \
+        if (m.n <= 4096) launch_any<GemvShape<1024, R, U, true, 4, true, 1, 2>>(m, a, MW); \
+        else launch_any<GemvShape<1024, R, U, true, 4, true, 4, 2>>(m, a, MW); }}
+    std::vector<Variant> vs = getenv("GB_T1K") ? std::vector<Variant>{
+        VPP("t512 r2 u4 pf pipe2 (product)", 4096, 512, 2, 4, 4),
+        VPK("t1024 r2 u4 pipe2 w4096", 4096, 2, 4),
+        VPK("t1024 r2 u4 pipe2 w3072", 3072, 2, 4),
+        VPK("t1024 r1 u4 pipe2 w4096", 4096, 1, 4),
+        VPK("t1024 r2 u2 pipe2 w4096", 4096, 2, 2),
+        VPP("t512 r2 u4 pf pipe2 w2048", 2048, 512, 2, 4, 2),
+    } : getenv("GB_PIPE") ? std::vector<Variant>{
         VPF("t512 r2 u4 pf (product)", 4096, 512, 2, 4),
         VPP("t512 r2 u4 pf pipe2", 4096, 512, 2, 4, 4),
         VPP("t512 r2 u2 pf pipe2", 4096, 512, 2, 2, 4),

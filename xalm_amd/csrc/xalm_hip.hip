@@ -153,6 +153,10 @@ struct xh_ctx {
     float* wo_part = nullptr;     // [n_kv_heads][dim]
     unsigned* ac_err = nullptr;   // sticky device flag
     int max_gemv_waves = 4096;  // 16 waves per CU
+    // the qkv launch: its whole matrix is one round at 16 waves per CU (every wave one group,
+    // requested at once); at 8 waves per CU each wave streams two groups back to back
+    // (tools/gemv_bench GB_T1K: 10.95 -> 10.12 us f16, 7.93 -> 7.34 us fp8)
+    int qkv_waves = 2048;
     // persistent engine (persistent.h)
     int engine = -1;            // -1 auto, 0 graph of kernels, 1 persistent, 2 stream (stream.h)
     int n_cu = 0;
@@ -581,7 +585,7 @@ int enqueue_step(xh_ctx* ctx, hipStream_t s, bool with_logits, bool greedy = fal
             if (rc != XH_E_INVALID) return set_err(ctx, rc, "layer %d: qkv + attention + Wo launch failed", l);
             ctx->qaw_ok = false;  // not instantiated / does not fit: the two-launch form from now on
         }
-        if (!launch_gemv<PRO_RMSNORM, EPI_QKV>(kdt(w.qkv_dt, w.qkv_x), qkv_args(ctx, l), s, mb))
+        if (!launch_gemv<PRO_RMSNORM, EPI_QKV>(kdt(w.qkv_dt, w.qkv_x), qkv_args(ctx, l), s, ctx->qkv_waves))
             return set_err(ctx, XH_E_INVALID, "layer %d: unsupported qkv dtype %d", l, w.qkv_dt);
         if (col) {
             // attention + Wo by columns (attn_col.h), W1/W3's rmsnorm sums the head partials
@@ -1276,6 +1280,7 @@ int xh_create(const xh_config* cfg, int device_ordinal, xh_ctx** out) {
     ctx->q_dim = c.n_heads * c.head_dim;
     ctx->kv_dim = c.n_kv_heads * c.head_dim;
     ctx->qpk = qpk;
+    if (const char* qw = getenv("XALM_QKV_WAVES")) ctx->qkv_waves = std::max(64, atoi(qw));  // launch-shape sweeps
     ctx->nsplit = attn_nsplit(c.n_kv_heads, c.max_seq_len);
     ctx->t_max = attn_split_len(c.max_seq_len, ctx->nsplit);
     ctx->t_max_aw = attn_split_len(c.max_seq_len, ctx->nsplit, attn_min_t_partials(c.head_dim, AW_THREADS));
