@@ -24,9 +24,13 @@ def load(pass_dir, counter):
 
 
 def main():
-    out = sys.argv[1]
-    fetch = load(os.path.join(out, "FETCH_SIZE"), "FETCH_SIZE")
-    write = load(os.path.join(out, "WRITE_SIZE"), "WRITE_SIZE")
+    # one or more pass directories (e.g. the f16 and the fp8 workload), merged per kernel name
+    fetch, write = defaultdict(list), defaultdict(list)
+    for out in sys.argv[1:]:
+        for k, v in load(os.path.join(out, "FETCH_SIZE"), "FETCH_SIZE").items():
+            fetch[k] += v
+        for k, v in load(os.path.join(out, "WRITE_SIZE"), "WRITE_SIZE").items():
+            write[k] += v
     res = {}
     for k in sorted(set(fetch) | set(write)):
         f = fetch.get(k, [])

@@ -4,7 +4,7 @@
 # Each GPU step has its own limit; a crash / abort / timeout ends the run.
 set -u
 cd "$(dirname "$0")/.."
-ROUND=${ROUND:-r01}
+ROUND=${ROUND:-r02}
 OUT=gpurun_out/$ROUND
 mkdir -p "$OUT"
 export TMPDIR=/tmp
@@ -17,12 +17,16 @@ step() {
     echo "== $name rc=$rc"
     if [ $rc -ne 0 ]; then tail -5 "$OUT/$name.log"; exit $rc; fi
 }
+step smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()"
+step pytest_gpu 900 python3 -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread -rs
 # HBM traffic (MI355X_MICROARCH.md HBM section): FETCH_SIZE and WRITE_SIZE in separate passes
 for c in FETCH_SIZE WRITE_SIZE; do
     step pmc_$c 300 rocprofv3 --pmc $c --kernel-trace -d "$OUT/pmc/$c" -o run --output-format csv -- \
         python3 bench.py --steps 16 --warmup 2 --no-cpu-baseline --kernel-iters 10 --prefill-tokens 0
+    step pmc_f8_$c 300 rocprofv3 --pmc $c --kernel-trace -d "$OUT/pmc_f8/$c" -o run --output-format csv -- \
+        python3 bench.py --workload mistral-7b-f8 --steps 16 --warmup 2 --no-cpu-baseline --kernel-iters 10 --prefill-tokens 0
 done
-python3 tools/pmc_summary.py "$OUT/pmc" > "$OUT/pmc.json"
+python3 tools/pmc_summary.py "$OUT/pmc" "$OUT/pmc_f8" > "$OUT/pmc.json"
 cp "$OUT/pmc.json" "profiles/${ROUND}_pmc.json"   # read by bench.py's roofline.traffic
 step kernel_trace 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
     python3 bench.py --steps 64 --warmup 4 --no-cpu-baseline --kernel-iters 50 --prefill-tokens 0
