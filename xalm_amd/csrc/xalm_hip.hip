@@ -585,7 +585,9 @@ int enqueue_step(xh_ctx* ctx, hipStream_t s, bool with_logits, bool greedy = fal
             if (rc != XH_E_INVALID) return set_err(ctx, rc, "layer %d: qkv + attention + Wo launch failed", l);
             ctx->qaw_ok = false;  // not instantiated / does not fit: the two-launch form from now on
         }
-        if (!launch_gemv<PRO_RMSNORM, EPI_QKV>(kdt(w.qkv_dt, w.qkv_x), qkv_args(ctx, l), s, ctx->qkv_waves))
+        // (gguf blocks take the unpipelined staged shape: every wave one group at 16 per CU)
+        if (!launch_gemv<PRO_RMSNORM, EPI_QKV>(kdt(w.qkv_dt, w.qkv_x), qkv_args(ctx, l), s,
+                                               gq_dt(w.qkv_dt) ? mb : ctx->qkv_waves))
             return set_err(ctx, XH_E_INVALID, "layer %d: unsupported qkv dtype %d", l, w.qkv_dt);
         if (col) {
             // attention + Wo by columns (attn_col.h), W1/W3's rmsnorm sums the head partials
