@@ -248,6 +248,19 @@ def test_pipelined_gemv_decode(wdt):
     assert np.abs(st.logits() - om.logits()).max() <= tol(om.logits())
 
 
+@pytest.mark.parametrize("wdt", [L.F8_E4M3, L.F8_E5M2, L.F16])
+def test_long_row_w2_decode(wdt):
+    # hidden 7168: W2 rows of 7 KiB (one-byte weights) / 14 KiB (f16) through the PF shape that
+    # holds x in 8 float4 per thread, partial last step (fp8: 7 chunks per row, steps of 4);
+    # token-loop logits vs the oracle at every position
+    gm, om = synthetic_pair(wdt, dim=256, hidden=7168, n_layers=1)
+    st = InferenceState(gm.config)
+    for pos, tok in enumerate([1, 17, 300, 5]):
+        gm.forward(st, tok, pos, L.OUTPUT_LOGITS)
+        om.forward(tok, pos)
+        assert np.abs(st.logits() - om.logits()).max() <= tol(om.logits()), pos
+
+
 @pytest.mark.parametrize("wdt", [L.F16, L.F8_E4M3])
 def test_fused_glu_split_is_bit_identical(wdt):
     # the fused GLU -> split-f16 epilogue and the two-launch route produce the same W2 input

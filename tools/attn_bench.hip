@@ -41,13 +41,16 @@ __global__ __launch_bounds__(THREADS) void k_signal(const AttnArgs a, unsigned* 
 int main(int argc, char** argv) {
     const int msl = 32768;
     const int kv_len = argc > 1 ? atoi(argv[1]) : 32768;
+    // slot pitch in fp16 elements (KVD + pad): how the ring's row pitch maps KV heads onto HBM channels
+    const int pad = argc > 2 ? atoi(argv[2]) : 0;
+    const int PITCH = KVD + pad;
     const int NC = 4;  // ring copies (4 x 128 MB) so the Infinity Cache serves nothing
     std::vector<uint16_t*> kc(NC), vc(NC);
     for (int c = 0; c < NC; c++) {
-        CK(hipMalloc(&kc[c], (size_t)msl * KVD * 2));
-        CK(hipMalloc(&vc[c], (size_t)msl * KVD * 2));
-        hipLaunchKernelGGL(fill16, dim3(2048), dim3(256), 0, 0, kc[c], (size_t)msl * KVD, 10 + c);
-        hipLaunchKernelGGL(fill16, dim3(2048), dim3(256), 0, 0, vc[c], (size_t)msl * KVD, 20 + c);
+        CK(hipMalloc(&kc[c], (size_t)msl * PITCH * 2));
+        CK(hipMalloc(&vc[c], (size_t)msl * PITCH * 2));
+        hipLaunchKernelGGL(fill16, dim3(2048), dim3(256), 0, 0, kc[c], (size_t)msl * PITCH, 10 + c);
+        hipLaunchKernelGGL(fill16, dim3(2048), dim3(256), 0, 0, vc[c], (size_t)msl * PITCH, 20 + c);
     }
     float *q, *po, *pml, *out;
     int* cnt;
@@ -71,7 +74,7 @@ int main(int argc, char** argv) {
     auto run = [&](auto kern, int threads, int nsplit, size_t smem, const char* name) {
         CK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
         AttnArgs a{};
-        a.q = q; a.kv_dim = KVD; a.n_heads = NH; a.nsplit = nsplit; a.part_o = po; a.part_ml = pml; a.sp = sp; a.out = out; a.counters = cnt;
+        a.q = q; a.kv_dim = PITCH; a.n_heads = NH; a.nsplit = nsplit; a.part_o = po; a.part_ml = pml; a.sp = sp; a.out = out; a.counters = cnt;
         std::vector<float> ts;
         for (int r = 0; r < 3; r++) {
             const int it = 20;
@@ -90,8 +93,10 @@ int main(int argc, char** argv) {
         const double bytes = 2.0 * kv_len * KVD * 2;
         printf("  %-22s nsplit %3d  %8.2f us  %7.1f GB/s\n", name, nsplit, ts[1], bytes / (ts[1] * 1e-6) / 1e9);
     };
-    printf("kv_len %d (%.1f MB of K+V)\n", kv_len, 2.0 * kv_len * KVD * 2 / 1e6);
+    printf("kv_len %d (%.1f MB of K+V), slot pitch %d\n", kv_len, 2.0 * kv_len * KVD * 2 / 1e6, PITCH);
+    const bool quick = argc > 3;
     for (int ns : {32, 64, 128}) {
+        if (quick && ns != 32) continue;
         const int T = attn_split_len(kv_len, ns, attn_min_t_partials(HD, 1024));
         run(k_round<1024>, 1024, ns, attn_smem_bytes(HD, QPK, T, ns, 1024), "round   t1024");
         run(k_signal<1024>, 1024, ns, attn_smem_bytes(HD, QPK, T, ns, 1024), "merged  t1024");

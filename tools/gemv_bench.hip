@@ -99,7 +99,19 @@ int main(int argc, char** argv) {
 #define VPK(NAME, MW, R, U) {NAME, [](const Mat& m, const GemvArgs& a) { \
         if (m.n <= 4096) launch_any<GemvShape<1024, R, U, true, 4, true, 1, 2>>(m, a, MW); \
         else launch_any<GemvShape<1024, R, U, true, 4, true, 4, 2>>(m, a, MW); }}
-    std::vector<Variant> vs = getenv("GB_T1K") ? std::vector<Variant>{
+    // W2-shaped (n = 14336) launch shapes: x in 8 float4 per thread; PIPE 2 needs n % (64 E U) == 0
+#define VW2(NAME, MW, R, U, P) {NAME, [](const Mat& m, const GemvArgs& a) { \
+        if (m.n > 4096) launch_any<GemvShape<512, R, U, true, 4, true, 8, P>>(m, a, MW); }}
+    std::vector<Variant> vs = getenv("GB_W2") ? std::vector<Variant>{
+        VW2("w2 r2 u4 (product)", 4096, 2, 4, 1),
+        VW2("w2 r2 u7", 4096, 2, 7, 1),
+        VW2("w2 r2 u7 pipe2", 4096, 2, 7, 2),
+        VW2("w2 r1 u7 pipe2", 4096, 1, 7, 2),
+        VW2("w2 r2 u2 pipe2", 4096, 2, 2, 2),
+        VW2("w2 r2 u4 pipe2 (f16 only)", 4096, 2, 4, 2),
+        VW2("w2 r1 u4", 4096, 1, 4, 1),
+        VW2("w2 r2 u7 pipe2 w2048", 2048, 2, 7, 2),
+    } : getenv("GB_T1K") ? std::vector<Variant>{
         VPP("t512 r2 u4 pf pipe2 (product)", 4096, 512, 2, 4, 4),
         VPK("t1024 r2 u4 pipe2 w4096", 4096, 2, 4),
         VPK("t1024 r2 u4 pipe2 w3072", 3072, 2, 4),
@@ -138,6 +150,8 @@ int main(int argc, char** argv) {
         for (size_t mi = 0; mi < mats.size(); mi++)
             for (size_t vi = 0; vi < vs.size(); vi++) {
                 const Mat& m = mats[mi];
+                if (getenv("GB_W2") && m.n <= 4096) continue;
+                if (getenv("GB_W2") && DT != XH_F16 && vs[vi].name.find("f16 only") != std::string::npos) continue;
                 if (m.n > 8192 && std::string(vs[vi].name).find("t128") == 0) continue;
                 GemvArgs a{};
                 a.row_bytes = (size_t)m.n * ESZ; a.n = m.n; a.rows = m.rows; a.x = x; a.norm_w = nw;
