@@ -372,6 +372,7 @@ __device__ __forceinline__ void attn_block(const AttnArgs& a, const int g, const
     constexpr int MG = (THREADS / NO < WAVES - 1 ? THREADS / NO : WAVES - 1) > 0
                            ? (THREADS / NO < WAVES - 1 ? THREADS / NO : WAVES - 1) : 1;
     constexpr int MB = 16;  // partial values per thread per round trip
+    static_assert(PARTIALS || NO <= THREADS, "merge: every output needs a thread of group 0");
     float* wts = sc;        // [QPK][n_active] weights (sc is free now)
     float* den_s = red + MG * NO;  // [QPK]; red[k * NO + idx]: group sums
     const int chunk = (n_active + MG - 1) / MG;
