@@ -82,7 +82,10 @@ def f16(a):
     return a.astype(np.float16).view(np.uint16)
 
 
-@pytest.mark.parametrize("head_dim,n_heads,n_kv", [(128, 32, 8), (128, 4, 1), (16, 4, 2), (64, 8, 8), (32, 8, 1)])
+# (256, 16, 2): 8 q heads per KV head x 256 = 2048 outputs per block, more than its 1024 threads
+# (the last split's merge covers them in rounds)
+@pytest.mark.parametrize("head_dim,n_heads,n_kv", [(128, 32, 8), (128, 4, 1), (16, 4, 2), (64, 8, 8), (32, 8, 1),
+                                                   (256, 16, 2)])
 @pytest.mark.parametrize("kv_len,msl", [(1, 64), (17, 64), (300, 4096), (4096, 4096), (100, 128)])
 def test_mha(head_dim, n_heads, n_kv, kv_len, msl):
     rng = np.random.default_rng(kv_len * 131 + head_dim + n_heads)

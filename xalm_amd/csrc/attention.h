@@ -372,7 +372,6 @@ __device__ __forceinline__ void attn_block(const AttnArgs& a, const int g, const
     constexpr int MG = (THREADS / NO < WAVES - 1 ? THREADS / NO : WAVES - 1) > 0
                            ? (THREADS / NO < WAVES - 1 ? THREADS / NO : WAVES - 1) : 1;
     constexpr int MB = 16;  // partial values per thread per round trip
-    static_assert(PARTIALS || NO <= THREADS, "merge: every output needs a thread of group 0");
     float* wts = sc;        // [QPK][n_active] weights (sc is free now)
     float* den_s = red + MG * NO;  // [QPK]; red[k * NO + idx]: group sums
     const int chunk = (n_active + MG - 1) / MG;
@@ -423,6 +422,16 @@ __device__ __forceinline__ void attn_block(const AttnArgs& a, const int g, const
                     if (j + k < j1) num = fmaf(w[j + k], pw[k], num);
             }
             red[mgrp * NO + midx] = num;
+        }
+        if constexpr (NO > THREADS) {
+            // more outputs than threads (one group): the rest one by one, all splits each
+            for (int idx = tid + THREADS; idx < NO; idx += THREADS) {
+                const float* w = wts + (idx / HD) * n_active;
+                const float* src = a.part_o + (size_t)g * NO + idx;
+                float n2 = 0.f;
+                for (int j = 0; j < n_active; j++) n2 = fmaf(w[j], ld_sc1(src + (size_t)j * mstride), n2);
+                red[idx] = n2;
+            }
         }
     }
     __syncthreads();
