@@ -454,6 +454,12 @@ __global__ void argmax_advance_kernel(const float* logits, int vocab, StepParams
     }
 }
 
+// wave cap of layer l's qkv launch: ctx->qkv_waves for the pipelined shape; gguf blocks take the
+// unpipelined staged shape, every wave one group at 16 waves per CU
+int qkv_launch_waves(const xh_ctx* ctx, int l) {
+    return gq_dt(ctx->L[l].qkv_dt) ? ctx->max_gemv_waves : ctx->qkv_waves;
+}
+
 bool use_attn_wo(const xh_ctx* ctx, int l) {
     const int dt = ctx->L[l].wo_dt;
     if (ctx->L[l].wo_x) return false;  // exact fp8 decode: the separate launches
@@ -585,9 +591,7 @@ int enqueue_step(xh_ctx* ctx, hipStream_t s, bool with_logits, bool greedy = fal
             if (rc != XH_E_INVALID) return set_err(ctx, rc, "layer %d: qkv + attention + Wo launch failed", l);
             ctx->qaw_ok = false;  // not instantiated / does not fit: the two-launch form from now on
         }
-        // (gguf blocks take the unpipelined staged shape: every wave one group at 16 per CU)
-        if (!launch_gemv<PRO_RMSNORM, EPI_QKV>(kdt(w.qkv_dt, w.qkv_x), qkv_args(ctx, l), s,
-                                               gq_dt(w.qkv_dt) ? mb : ctx->qkv_waves))
+        if (!launch_gemv<PRO_RMSNORM, EPI_QKV>(kdt(w.qkv_dt, w.qkv_x), qkv_args(ctx, l), s, qkv_launch_waves(ctx, l)))
             return set_err(ctx, XH_E_INVALID, "layer %d: unsupported qkv dtype %d", l, w.qkv_dt);
         if (col) {
             // attention + Wo by columns (attn_col.h), W1/W3's rmsnorm sums the head partials
@@ -2174,7 +2178,8 @@ int xh_time_kernel(xh_ctx* ctx, int which, int iters, float* avg_us) {
         const int l = rot++ % ctx->c.n_layers;
         switch (which) {
             case 0: return launch_gemv<PRO_RMSNORM, EPI_GLU>(kdt(ctx->L[l].w13_dt, ctx->L[l].w13_x), w13_args(ctx, l), ctx->stream, mb);
-            case 1: return launch_gemv<PRO_RMSNORM, EPI_QKV>(kdt(ctx->L[l].qkv_dt, ctx->L[l].qkv_x), qkv_args(ctx, l), ctx->stream, mb);
+            case 1: return launch_gemv<PRO_RMSNORM, EPI_QKV>(kdt(ctx->L[l].qkv_dt, ctx->L[l].qkv_x), qkv_args(ctx, l), ctx->stream,
+                                                             qkv_launch_waves(ctx, l));
             case 2: return launch_gemv<PRO_PLAIN, EPI_RESID>(kdt(ctx->L[l].wo_dt, ctx->L[l].wo_x), wo_args(ctx, l), ctx->stream, mb);
             case 3: return launch_gemv<PRO_PLAIN, EPI_RESID>(kdt(ctx->L[l].w2_dt, ctx->L[l].w2_x), w2_args(ctx, l), ctx->stream, mb);
             case 4: return launch_gemv<PRO_RMSNORM, EPI_LOGITS>(kdt(ctx->wcls_dt, ctx->wcls_x), cls_args(ctx), ctx->stream, mb);
