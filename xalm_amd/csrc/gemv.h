@@ -456,6 +456,36 @@ __device__ __forceinline__ void gemv_chunk_gq(const char* wrow, const size_t row
     }
 }
 
+// gguf blocks, split in two for the pipelined stream: the f16 block scale d of each of the
+// chunks [it, it+U) of a row group (wrow: this lane's pointer into the group's first row)...
+template <int DT, int ROWS, int U>
+__device__ __forceinline__ void gq_load_scales(float (&d)[U][ROWS], const char* wrow, const size_t row_bytes,
+                                               const size_t qbytes, const int it, const int lane) {
+    constexpr int E = WDec<DT>::E;
+    const char* rb = wrow - lane * 16 + qbytes;
+#pragma unroll
+    for (int u = 0; u < U; u++)
+#pragma unroll
+        for (int r = 0; r < ROWS; r++) {
+            const int blk = (((it + u) * 64 + lane) * E) / WScale<DT>::BLOCK;
+            d[u][r] = (float)__builtin_bit_cast(_Float16, *(const uint16_t*)(rb + (size_t)r * row_bytes + blk * 2));
+        }
+}
+// ...and the scaled chunk sums against the staged x, as gemv_chunk_gq
+template <int DT, int ROWS, int U>
+__device__ __forceinline__ void gq_compute(const u32x4 (&wv)[U][ROWS], const float (&d)[U][ROWS], const float4* xs4,
+                                           const int it, const int lane, float* acc) {
+    constexpr int QN = WDec<DT>::E / 4;
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        float4 xv[QN];
+#pragma unroll
+        for (int qd = 0; qd < QN; qd++) xv[qd] = xs4[((it + u) * QN + qd) * 64 + lane];
+#pragma unroll
+        for (int r = 0; r < ROWS; r++) acc[r] = fmaf(d[u][r], gq_dot<DT>(wv[u][r], xv), acc[r]);
+    }
+}
+
 // Row group `grp` of the matrix: lane pointer and row stride (0 for the duplicated last row
 // of an odd row count: rows past the end re-read the last row and are never stored).
 template <int ROWS>
@@ -537,31 +567,38 @@ __device__ __forceinline__ void gemv_rows(const GemvArgs& a, int g, const int to
 // multiplied, so a wave keeps U to 2U chunks per row in flight instead of draining to zero at
 // every step, and a group's reduction and epilogue run behind the next group's loads.
 // FIRST: the first group's step 0 is already in `pre`.
+// gguf blocks (GQ): every step also loads its chunks' block scales (a second register set),
+// and `pre_d` holds the first step's scales.
 template <int DT, int EPI, class S, bool FIRST, bool SC1 = false>
 __device__ __forceinline__ void gemv_rows_pipe(const GemvArgs& a, const int g0, const int total_waves, const int lane,
                                                const float4* xs4, const u32x4 (&pre)[S::U][S::ROWS],
-                                               unsigned long long* best = nullptr) {
+                                               unsigned long long* best = nullptr,
+                                               const float (*pre_d)[S::ROWS] = nullptr) {
     constexpr int ROWS = S::ROWS, U = S::U;
     constexpr int E = WDec<DT>::E;
+    constexpr bool GQ = WScale<DT>::BLOCK > 0;
     const int n_groups = gemv_groups<S>(a);
     if (g0 >= n_groups) return;
     const int steps = a.n / (64 * E * U);
+    const size_t qb = GQ ? gq_qbytes(DT, (size_t)a.n) : 0;
     // step k of this wave: group g0 + (k / steps) * total_waves, chunks from (k % steps) * U
     const int total = ((n_groups - g0 + total_waves - 1) / total_waves) * steps;
-    auto load = [&](u32x4 (&w)[U][ROWS], const int k) {
+    auto load = [&](u32x4 (&w)[U][ROWS], float (&d)[U][ROWS], const int k) {
         const int q = k / steps;
         size_t rs;
         const char* wrow = gemv_row_ptr<ROWS>(a, g0 + q * total_waves, lane, rs);
         gemv_load<ROWS, U, S::NT>(w, wrow, rs, (k - q * steps) * U);
+        if constexpr (GQ) gq_load_scales<DT, ROWS, U>(d, wrow, rs, qb, (k - q * steps) * U, lane);
     };
     float acc[ROWS];
 #pragma unroll
     for (int r = 0; r < ROWS; r++) acc[r] = 0.f;
     // multiply step k's chunks; after a group's last step, its reduction and epilogue
-    auto step = [&](const u32x4 (&w)[U][ROWS], const int k) {
+    auto step = [&](const u32x4 (&w)[U][ROWS], const float (&d)[U][ROWS], const int k) {
         const int q = k / steps;
         const int it = (k - q * steps) * U;
-        gemv_compute<DT, ROWS, U>(w, xs4, it, lane, acc);
+        if constexpr (GQ) gq_compute<DT, ROWS, U>(w, d, xs4, it, lane, acc);
+        else gemv_compute<DT, ROWS, U>(w, xs4, it, lane, acc);
         if (it + U == steps * U) {
 #pragma unroll
             for (int r = 0; r < ROWS; r++) acc[r] = wave_sum(acc[r]);
@@ -571,28 +608,32 @@ __device__ __forceinline__ void gemv_rows_pipe(const GemvArgs& a, const int g0, 
         }
     };
     u32x4 wa[U][ROWS], wb[U][ROWS];
+    float da[U][ROWS], db[U][ROWS];  // GQ only (otherwise unused)
     if constexpr (FIRST) {
 #pragma unroll
         for (int u = 0; u < U; u++)
 #pragma unroll
-            for (int r = 0; r < ROWS; r++) wa[u][r] = pre[u][r];
+            for (int r = 0; r < ROWS; r++) {
+                wa[u][r] = pre[u][r];
+                if constexpr (GQ) da[u][r] = pre_d[u][r];
+            }
     } else {
-        load(wa, 0);
+        load(wa, da, 0);
     }
     // the loads stay outside any branch, so the compiler's waits count only the older set
     int k = 0;
     for (; k + 2 < total; k += 2) {
-        load(wb, k + 1);
-        step(wa, k);
-        load(wa, k + 2);
-        step(wb, k + 1);
+        load(wb, db, k + 1);
+        step(wa, da, k);
+        load(wa, da, k + 2);
+        step(wb, db, k + 1);
     }
     if (k + 1 < total) {
-        load(wb, k + 1);
-        step(wa, k);
-        step(wb, k + 1);
+        load(wb, db, k + 1);
+        step(wa, da, k);
+        step(wb, db, k + 1);
     } else {
-        step(wa, k);
+        step(wa, da, k);
     }
 }
 
@@ -687,20 +728,27 @@ __global__ __launch_bounds__(S::THREADS, S::MINW) void gemv_kernel(const GemvArg
     if (a.aw_reset && blockIdx.x == 0 && threadIdx.x < 9) a.aw_reset[32 * threadIdx.x] = 0u;
     unsigned long long best = 0;  // EPI_LOGITS: this wave's best candidate (lane 0)
 
-    if constexpr (S::PF && WScale<DT>::BLOCK == 0) {  // gguf blocks: the staged form below
+    // gguf blocks: the pipelined PF shapes (block scales loaded beside the codes), else staged
+    if constexpr (S::PF && (WScale<DT>::BLOCK == 0 || S::PIPE == 2)) {
         float4 xv[S::XN], nw[S::XN];
         stage_x_issue<PRO, S>(a, xv, nw);
         // unconditional (a wave past the last group re-reads that group's chunks, unused)
         const int n_groups = gemv_groups<S>(a);
         const bool prefetched = g < n_groups;
         u32x4 pre[S::U][S::ROWS];
+        float pre_d[S::U][S::ROWS];
         gemv_prefetch<S>(a, min(g, n_groups - 1), lane, pre);
+        if constexpr (WScale<DT>::BLOCK > 0) {
+            size_t rs;
+            const char* wrow = gemv_row_ptr<S::ROWS>(a, min(g, n_groups - 1), lane, rs);
+            gq_load_scales<DT, S::ROWS, S::U>(pre_d, wrow, rs, gq_qbytes(DT, (size_t)a.n), 0, lane);
+        }
         stage_x_finish<E, PRO, S>(a, xv, nw, xs4, red);
         if (EPI == EPI_QKV && blockIdx.x == 0) rotate_sinks<S::THREADS>(a, a.sp->kv_sink);
         __syncthreads();
         if (a.trace && threadIdx.x == 0) a.trace[4 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
         if constexpr (S::PIPE == 2) {
-            if (prefetched) gemv_rows_pipe<DT, EPI, S, true>(a, g, gridDim.x * S::WAVES, lane, xs4, pre, &best);
+            if (prefetched) gemv_rows_pipe<DT, EPI, S, true>(a, g, gridDim.x * S::WAVES, lane, xs4, pre, &best, pre_d);
         } else {
             if (prefetched) gemv_rows<DT, EPI, S, true>(a, g, gridDim.x * S::WAVES, lane, xs4, pre, &best);
             else gemv_rows<DT, EPI, S, false>(a, g, gridDim.x * S::WAVES, lane, xs4, pre, &best);

@@ -283,6 +283,14 @@ void launch_gemv_t(const GemvArgs& a, hipStream_t s, int max_waves) {
         if (pf && a.n / 4 <= 2 * 512 && a.n % (64 * E * UNROLL) == 0)
             return launch_gemv_s<DT, PRO, EPI, ShapePF2P>(a, s, max_waves);
     }
+    if constexpr ((EPI == EPI_QKV || EPI == EPI_GLU) && gq_dt(DT)) {
+        // gguf blocks: the pipelined PF shape with the block scales loaded beside the codes;
+        // Q4_0 rows of a 4096-wide input are 2 chunks, so 2 chunks per step
+        constexpr int UG = DT == XH_Q4_0 ? 2 : UNROLL;
+        using ShapeGQ = GemvShape<512, ROWS, UG, true, 4, true, 2, 2>;
+        if (a.n % 4 == 0 && a.n / 4 <= 2 * 512 && a.n % (64 * E * UG) == 0)
+            return launch_gemv_s<DT, PRO, EPI, ShapeGQ>(a, s, max_waves);
+    }
     if (pf && a.n / 4 <= 2 * 512) launch_gemv_s<DT, PRO, EPI, ShapePF2>(a, s, max_waves);
     else if constexpr (PRO == PRO_PLAIN) {
         if (pf && a.n / 4 <= 8 * 512) launch_gemv_s<DT, PRO, EPI, ShapePF8>(a, s, max_waves);
