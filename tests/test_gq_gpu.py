@@ -87,11 +87,13 @@ def test_forward_on_converter_blocks(name, fuse):
     om.close()
 
 
+@pytest.mark.parametrize("dim,hidden,layers", [(2048, 4096, 2), (4096, 2048, 1)])
 @pytest.mark.parametrize("dtype", GQ)
-def test_synthetic_blocks_forward(dtype):
+def test_synthetic_blocks_forward(dtype, dim, hidden, layers):
     # device-generated blocks (synth_gq_kernel) equal the oracle's (xo_fill_synthetic): the
-    # logits agree; dims that take the long-row matvec shapes
-    w = dict(dim=2048, hidden=4096, layers=2, heads=16, kv_heads=4, head_dim=128, vocab=1000, msl=256,
+    # logits agree; dims that take the long-row matvec shapes, and (dim 4096) the pipelined
+    # block shapes for qkv, W1/W3 and lm_head (n = 4096) and Wo / W2 (n = 2048)
+    w = dict(dim=dim, hidden=hidden, layers=layers, heads=16, kv_heads=4, head_dim=128, vocab=1000, msl=256,
              theta=1e6, wdt=dtype, edt=dtype, cdt=dtype)
     c = bench.make_config(w)
     gm, om = Model(c), O.OracleModel(c)

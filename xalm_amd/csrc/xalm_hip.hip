@@ -283,13 +283,20 @@ void launch_gemv_t(const GemvArgs& a, hipStream_t s, int max_waves) {
         if (pf && a.n / 4 <= 2 * 512 && a.n % (64 * E * UNROLL) == 0)
             return launch_gemv_s<DT, PRO, EPI, ShapePF2P>(a, s, max_waves);
     }
-    if constexpr ((EPI == EPI_QKV || EPI == EPI_GLU) && gq_dt(DT)) {
-        // gguf blocks: the pipelined PF shape with the block scales loaded beside the codes;
-        // Q4_0 rows of a 4096-wide input are 2 chunks, so 2 chunks per step
+    if constexpr (gq_dt(DT)) {
+        // gguf blocks: the pipelined PF shapes with the block scales loaded beside the codes.
+        // Q4_0 rows of a 4096-wide input are 2 chunks, so 2 chunks per step; W2-long inputs
+        // (14336: 14 / 7 chunks per row) step by 2 (Q8_0) / 1 (Q4_0) chunks
         constexpr int UG = DT == XH_Q4_0 ? 2 : UNROLL;
         using ShapeGQ = GemvShape<512, ROWS, UG, true, 4, true, 2, 2>;
         if (a.n % 4 == 0 && a.n / 4 <= 2 * 512 && a.n % (64 * E * UG) == 0)
             return launch_gemv_s<DT, PRO, EPI, ShapeGQ>(a, s, max_waves);
+        if constexpr (PRO == PRO_PLAIN) {
+            constexpr int UL = DT == XH_Q4_0 ? 1 : 2;
+            using ShapeGQL = GemvShape<512, ROWS, UL, true, 4, true, 8, 2>;
+            if (a.n % 4 == 0 && a.n / 4 <= 8 * 512 && a.n % (64 * E * UL) == 0)
+                return launch_gemv_s<DT, PRO, EPI, ShapeGQL>(a, s, max_waves);
+        }
     }
     if (pf && a.n / 4 <= 2 * 512) launch_gemv_s<DT, PRO, EPI, ShapePF2>(a, s, max_waves);
     else if constexpr (PRO == PRO_PLAIN) {
