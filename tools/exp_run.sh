@@ -1,8 +1,6 @@
 set -u
 O=gpurun_out/exp; mkdir -p $O
-r() { local n=$1; shift; echo "== $n"; timeout -k 10 600 "$@" > $O/$n.log 2>&1; local rc=$?; tail -1 $O/$n.log | cut -c1-120; [ $rc -eq 0 ] || { echo "rc=$rc"; tail -40 $O/$n.log; exit $rc; }; }
-r test_gq python -u -m pytest tests/test_gq_gpu.py -m gpu -x -q --timeout 300 --timeout-method thread
-for i in 1 2; do
-  unset XALM_HIP_LIB; r q4_new_$i python bench.py --workload mistral-7b-q4_0 --no-cpu-baseline --prefill-tokens 0
-  export XALM_HIP_LIB=xalm_amd/lib/var_q4base.so; r q4_base_$i python bench.py --workload mistral-7b-q4_0 --no-cpu-baseline --prefill-tokens 0
-done
+r() { local n=$1; shift; echo "== $n"; timeout -k 10 900 "$@" > $O/$n.log 2>&1; local rc=$?; tail -1 $O/$n.log | cut -c1-160; [ $rc -eq 0 ] || { echo "rc=$rc"; tail -40 $O/$n.log; exit $rc; }; }
+r smoke python -c "import __graft_entry__ as g; g.smoke()"
+r tests python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread -rs
+r bench python bench.py
