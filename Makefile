@@ -26,8 +26,7 @@ endif
 oracle:
 	$(MAKE) -C oracle
 
-# the persistent and fused attention + Wo kernels are instantiated per weight dtype in their own
-# objects (parallel build)
+# the fused attention + Wo kernel is instantiated per Wo dtype in its own objects (parallel build)
 OBJ := xalm_amd/build
 PK_DTS := 1 2 3 6 7 9
 PK_OBJS := $(patsubst %,$(OBJ)/dt_launch_dt%.o,$(PK_DTS))
@@ -37,12 +36,7 @@ $(OBJ)/xalm_hip.o: $(HIP_SRC) $(HIP_HDR)
 $(OBJ)/dt_launch_dt%.o: xalm_amd/csrc/dt_launch.hip $(HIP_HDR)
 	@mkdir -p $(OBJ)
 	$(HIPCC) $(HIPFLAGS) -DPK_DT=$* -c -o $@ $<
-SE_DTS := 1 2 3 6 7
-SE_OBJS := $(patsubst %,$(OBJ)/se_launch_dt%.o,$(SE_DTS))
-$(OBJ)/se_launch_dt%.o: xalm_amd/csrc/se_launch.hip $(HIP_HDR)
-	@mkdir -p $(OBJ)
-	$(HIPCC) $(HIPFLAGS) -DSE_DT=$* -c -o $@ $<
-$(LIB)/libxalm_hip.so: $(OBJ)/xalm_hip.o $(PK_OBJS) $(SE_OBJS)
+$(LIB)/libxalm_hip.so: $(OBJ)/xalm_hip.o $(PK_OBJS)
 	@mkdir -p $(LIB)
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $^
 

@@ -144,46 +144,126 @@ def job_value(world, steps, elapsed):
     return world * steps / elapsed
 
 
-def cpu_baseline(w, c, prompt, gpu_logits0, gpu_tokens, n_decode):
-    """Oracle (restated src/infer.cpp, OpenMP) on the same weights, bounded sample."""
+def host_cpu_info():
+    """lscpu model name, physical cores of the host, and the CPUs this process may run on (the
+    GPU box gives one GPU's share of the host: OMP_NUM_THREADS and the affinity mask say how many)."""
+    info = {"model": None, "physical_cores": None, "logical_cpus": os.cpu_count(),
+            "affinity_cpus": len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None}
+    try:
+        import subprocess
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=20).stdout
+        kv = {}
+        for line in out.splitlines():
+            if ":" in line:
+                k, v = line.split(":", 1)
+                kv[k.strip()] = v.strip()
+        info["model"] = kv.get("Model name")
+        sockets, cores = int(kv.get("Socket(s)", "0") or 0), int(kv.get("Core(s) per socket", "0") or 0)
+        info["physical_cores"] = sockets * cores or None
+    except Exception:  # lscpu missing: the fields stay null
+        pass
+    return info
+
+
+def cpu_baseline(w, c, prompt, gpu_logits0, gpu_tokens, n_decode, one_thread_tokens=2):
+    """The reference -d cpu path (the oracle: src/infer.cpp restated, OpenMP over matvec rows and
+    heads as src/infer.cpp:118 / :438) on the same synthetic weights, timed on this host: hydrate
+    the prompt, then `n_decode` decode tokens teacher-forced on the GPU's tokens (run_completion
+    -m completion -n N, src/main.cpp:94-115), as wall tok/s and as the reference's own statistic
+    (prompt + generated) / (user + sys CPU s) (src/main.cpp:117-127, src/profiler.h:124-129; NOT
+    wall clock).  Parity of the same run: GPU logits after the prompt vs the oracle's, next to
+    the oracle's own sensitivity to the in-row summation order (8-wide FMA lanes vs sequential,
+    both valid readings of the reference's `omp simd` loop)."""
+    import resource
+
     from oracle import oracle as O
     t_gen = time.time()
+    weights = [(kind, layer, dt, O.synthetic(*tensor_shape(c, kind), dt, seed, mean, std))
+               for kind, layer, dt, seed, mean, std in tensor_specs(w)]
     om = O.OracleModel(c)
-    for kind, layer, dt, seed, mean, std in tensor_specs(w):
-        rows, cols = tensor_shape(c, kind)
-        om.set_tensor(kind, layer, dt, O.synthetic(rows, cols, dt, seed, mean, std))
+    for kind, layer, dt, arr in weights:
+        om.set_tensor(kind, layer, dt, arr)
+    pos0, hyd = 0, prompt
     if w["kv_prefill"]:
-        return None  # the CPU sample is defined on the 4k-context workloads only
+        kv_dim = c.n_kv_heads * c.head_dim
+        for layer in range(c.n_layers):
+            for which in (0, 1):
+                om.set_kv(layer, which, 0, O.synthetic(w["kv_prefill"], kv_dim, L.F16, 5000 + 2 * layer + which,
+                                                       0.0, 1.0))
+        pos0, hyd = w["kv_prefill"], prompt[:1]
     t_gen = time.time() - t_gen
-    for pos, tok in enumerate(prompt):
-        om.forward(tok, pos, L.OUTPUT_LOGITS if pos == len(prompt) - 1 else L.HYDRATE_KV_CACHE)
+    threads = O.num_threads()
+    ru0 = resource.getrusage(resource.RUSAGE_SELF)
+    t0 = time.time()
+    for i, tok in enumerate(hyd):
+        om.forward(tok, pos0 + i, L.OUTPUT_LOGITS if i == len(hyd) - 1 else L.HYDRATE_KV_CACHE)
+    t_hyd = time.time() - t0
     lg0 = om.logits()
     parity_max_abs = float(np.abs(lg0 - gpu_logits0).max())
     # teacher-forced on the GPU's tokens so both sides see identical inputs
-    pos = len(prompt)
-    agree = 0
-    t0 = time.time()
+    pos = pos0 + len(hyd)
+    agree, disagree = 0, []
+    t1 = time.time()
     for i in range(n_decode):
-        agree += int(O.sample_argmax(om.logits()) == gpu_tokens[i])
+        lg = om.logits()
+        ref_tok = O.sample_argmax(lg)
+        if ref_tok == gpu_tokens[i]:
+            agree += 1
+        else:  # the logit gap the two paths saw at this step (a near-tie if below the error)
+            disagree.append({"step": i, "gpu": int(gpu_tokens[i]), "oracle": int(ref_tok),
+                             "oracle_logit_gap": float(lg[ref_tok] - lg[gpu_tokens[i]])})
         om.forward(gpu_tokens[i], pos, L.OUTPUT_LOGITS)
         pos += 1
-    dt = time.time() - t0
-    # SURVEY §8d also asks for a 1-thread run: one more teacher-forced token on one thread
-    threads = O.num_threads()
+    t_dec = time.time() - t1
+    ru1 = resource.getrusage(resource.RUSAGE_SELF)
+    cpu_s = (ru1.ru_utime - ru0.ru_utime) + (ru1.ru_stime - ru0.ru_stime)
+    # one-thread sample (SURVEY §8d): a couple more teacher-forced tokens on one thread
     O.set_threads(1)
-    t1 = time.time()
-    om.forward(gpu_tokens[n_decode], pos, L.OUTPUT_LOGITS)
-    one = time.time() - t1
+    t2 = time.time()
+    for i in range(one_thread_tokens):
+        om.forward(gpu_tokens[n_decode + i], pos, L.OUTPUT_LOGITS)
+        pos += 1
+    one = (time.time() - t2) / one_thread_tokens
     O.set_threads(threads)
-    return dict(value=n_decode / dt, unit="tok/s", cores=threads, kind="port",
-                one_thread={"value": 1.0 / one, "unit": "tok/s", "cores": 1, "sample": "1 decode token"},
-                sample=f"{n_decode} greedy decode tokens after a {len(prompt)}-token hydrate, full "
-                       f"{w['desc'].split(',')[0]} shapes, same synthetic weights (wall clock, "
-                       f"OpenMP oracle/xalm_oracle.c)",
-                ms_per_token=1000 * dt / n_decode, weight_gen_s=round(t_gen, 2),
+    # order sensitivity: the same prompt on a fresh oracle with sequential in-row sums (the
+    # prompt only: a 32k history is the same rows either way)
+    order = None
+    if not w["kv_prefill"] and w["wdt"] == L.F16:
+        om.close()
+        om2 = O.OracleModel(c)
+        for kind, layer, dt, arr in weights:
+            om2.set_tensor(kind, layer, dt, arr)
+        O.set_matmul_order(1)
+        for i, tok in enumerate(hyd):
+            om2.forward(tok, i, L.OUTPUT_LOGITS if i == len(hyd) - 1 else L.HYDRATE_KV_CACHE)
+        O.set_matmul_order(0)
+        lg_seq = om2.logits()
+        om2.close()
+        order = {"oracle_lanes_vs_sequential_max_abs": float(np.abs(lg0 - lg_seq).max()),
+                 "gpu_vs_oracle_sequential_max_abs": float(np.abs(gpu_logits0 - lg_seq).max())}
+    cpu = host_cpu_info()
+    return dict(value=round(n_decode / t_dec, 3), unit="tok/s", cores=threads, kind="port",
+                cpu_model=cpu["model"], host_physical_cores=cpu["physical_cores"],
+                host_logical_cpus=cpu["logical_cpus"], affinity_cpus=cpu["affinity_cpus"],
+                threads_note="OpenMP threads = this process's CPU share on the GPU box (OMP_NUM_THREADS / "
+                             "affinity), not the host's physical core count",
+                sample=f"-m completion -n {n_decode} equivalent: {len(hyd)}-token hydrate"
+                       + (f" at pos {pos0} over a {w['kv_prefill']}-slot history" if w["kv_prefill"] else "")
+                       + f", then {n_decode} greedy decode tokens teacher-forced on the GPU's tokens, full "
+                       f"{w['desc'].split(',')[0]} shapes, same synthetic weights (wall clock, OpenMP "
+                       "oracle/xalm_oracle.c = the reference's CPU algorithm restated)",
+                ms_per_token=round(1000 * t_dec / n_decode, 2),
+                hydrate_s=round(t_hyd, 3), weight_gen_s=round(t_gen, 2),
+                reference_stat={"value": round((len(hyd) + n_decode) / cpu_s, 3) if cpu_s > 0 else None,
+                                "unit": "tok/s", "definition": "(prompt + generated) / (user + sys CPU s), "
+                                "src/main.cpp:117-127 + src/profiler.h:124-129; NOT wall clock",
+                                "user_sys_s": round(cpu_s, 2)},
+                one_thread={"value": round(1.0 / one, 3), "unit": "tok/s", "cores": 1,
+                            "sample": f"{one_thread_tokens} teacher-forced decode tokens"},
                 parity={"logits_max_abs_after_prompt": parity_max_abs,
                         "logits_scale": float(np.abs(lg0).max()),
-                        "greedy_tokens_agree": f"{agree}/{n_decode}"})
+                        "order_sensitivity": order,
+                        "greedy_tokens_agree": f"{agree}/{n_decode}", "disagreements": disagree[:16]})
 
 
 def main():
@@ -192,21 +272,17 @@ def main():
     ap.add_argument("--steps", type=int, default=256)
     ap.add_argument("--warmup", type=int, default=8)
     ap.add_argument("--workload", default="mistral-7b-f16", choices=sorted(WORKLOADS))
-    ap.add_argument("--cpu-tokens", type=int, default=4)
+    ap.add_argument("--cpu-tokens", type=int, default=128,
+                    help="CPU baseline decode tokens (-m completion -n N; 32k workload: min(N, 32))")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--kernel-iters", type=int, default=200)
-    ap.add_argument("--engine", type=int, default=-1, choices=(-1, 0, 1, 2),
-                    help="-1 auto, 0 graph of kernels, 1 persistent kernel, 2 stream kernel (LDS-DMA weight ring)")
     ap.add_argument("--prefill-mode", type=int, default=1, choices=(1, 2, 3),
                     help="batched prefill GEMMs (XH_OPT_PREFILL): 1 default per dtype, 2 split-f16 MFMA "
                          "wherever the weights allow, 3 f32-input MFMA only")
     ap.add_argument("--prefill-tokens", type=int, default=512,
                     help="also time xh_prefill of this many prompt tokens (batched f32-MFMA path; 0 = skip)")
-    ap.add_argument("--fuse-attn-wo", type=int, default=1, choices=(0, 1, 2),
-                    help="graph engine: qkv + attention + Wo in one launch (2), attention + Wo (1), none (0)")
-    ap.add_argument("--col-kv-max", type=int, default=-1,
-                    help="XH_OPT_COL_KV_MAX: histories up to this take the column-form attention + Wo "
-                         "(-1 = library default, 0 = off)")
+    ap.add_argument("--fuse-attn-wo", type=int, default=1, choices=(0, 1),
+                    help="attention + Wo in one launch (1) or two launches (0)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -228,12 +304,7 @@ def main():
     for kind, layer, dt, seed, mean, std in tensor_specs(w):
         model.upload_synthetic(kind, layer, dt, seed, mean, std)
 
-    model.set_engine(args.engine)
     model.set_option(L.OPT_FUSE_ATTN_WO, args.fuse_attn_wo)
-    if args.col_kv_max >= 0:
-        model.set_option(L.OPT_COL_KV_MAX, args.col_kv_max)
-    col_max = model.get_option(L.OPT_COL_KV_MAX) if model.engine == 0 else 0
-    engine = model.engine
     prompt = prompt_tokens(c.vocab_size)
     st = InferenceState(c)
     pos0 = 0
@@ -253,7 +324,6 @@ def main():
         raise SystemExit(f"steps exceed the {c.max_seq_len} context")
 
     toks, elapsed = timed_region(dist, torch_mod, lambda: model.decode_greedy(pos, args.steps))
-    launch_us = model.last_launch_us() if engine in (1, 2) else None
     assert len(toks) == args.steps
 
     # algorithmic bytes of the timed tokens: Model::active_bytes(pos) (src/model.cpp:12-35)
@@ -262,17 +332,11 @@ def main():
 
     # graph engine's kernels, each timed on its own (HIP events on the context stream)
     kv_len_now = min(c.max_seq_len, pos + args.steps)
-    # every timed step in the column form (history <= col_max): its W1/W3 launch sums the
-    # per-head Wo partials in the rmsnorm prologue (which 7), else the plain one (which 0)
-    col_all = col_max > 0 and kv_len_now <= col_max
-    w13_which = 7 if col_all else 0
-    k_us = model.time_kernel(w13_which, args.kernel_iters)
-    k_bytes = model.kernel_bytes(w13_which, kv_len_now)
+    k_us = model.time_kernel(0, args.kernel_iters)
+    k_bytes = model.kernel_bytes(0, kv_len_now)
     k_gbps = k_bytes / (k_us * 1e-6) / 1e9
     extra_kernels = {"gemv_w13": {"avg_us": round(k_us, 2), "GBps": round(k_gbps, 1)}}
     timed = [(1, "gemv_qkv"), (2, "gemv_wo"), (3, "gemv_w2"), (4, "gemv_lm_head"), (5, "attention")]
-    if col_max > 0:
-        timed.append((6, "attn_wo_col"))
     for which, name in timed:
         us = model.time_kernel(which, max(20, args.kernel_iters // 4))
         b = model.kernel_bytes(which, kv_len_now)
@@ -313,31 +377,20 @@ def main():
                                  "finite": bool(np.isfinite(np.log(probs)).all())}
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and not w["kv_prefill"]:
-        n = min(args.cpu_tokens, len(warm_tokens) - 1) if warm_tokens else 0  # +1 token: the 1-thread sample
-        if n:
-            cpu = cpu_baseline(w, c, prompt, logits0, warm_tokens, n)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        seq = list(warm_tokens) + list(toks)  # the GPU's greedy tokens after the prompt
+        n = min(args.cpu_tokens, 32 if w["kv_prefill"] else args.cpu_tokens, len(seq) - 2)  # +2: 1-thread
+        if n > 0:
+            cpu = cpu_baseline(w, c, prompt, logits0, seq, n)
 
-    if engine in (1, 2):
-        # dominant (only) kernel: the one-launch decode kernel; one launch = the K timed tokens
-        r_gbps = step_bytes / (launch_us * 1e-6) / 1e9
-        kname = "persistent_decode_kernel" if engine == 1 else "stream_decode_kernel"
-        roofline = {"bound": "hbm", "achieved": round(r_gbps, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                    "frac": round(r_gbps / HBM_PEAK_GBPS, 4), "traffic": None,
-                    "kernel": kname + " (all phases of all timed tokens, one launch)",
-                    "bytes_per_launch": step_bytes, "avg_launch_us": round(launch_us, 1)}
-    else:
-        # the W1/W3 launch's exact instantiation (PF shape, see xalm_hip.hip launch_gemv_t)
-        # (the pipelined PF shape, PIPE = 2)
-        traffic, src = pmc_traffic("void xalm::gemv_kernel<%d, %d, 3, xalm::GemvShape<512, 2, 4, true, 4, true, 2, 2> >"
-                                   % (w["wdt"], 2 if col_all else 1))
-        roofline = {"bound": "hbm", "achieved": round(k_gbps, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                    "frac": round(k_gbps / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                    "traffic_source": src,
-                    "kernel": ("gemv_kernel<PRO_RMSNORM_P,EPI_GLU> (fused W1/W3 + sum of the Wo partials + rmsnorm + "
-                               "silu*up)" if col_all else
-                               "gemv_kernel<PRO_RMSNORM,EPI_GLU> (fused W1/W3 + rmsnorm + silu*up)") + ", layer 0",
-                    "bytes_per_launch": k_bytes, "avg_launch_us": round(k_us, 2)}
+    # the W1/W3 launch's exact instantiation (the pipelined PF shape, PIPE = 2)
+    traffic, src = pmc_traffic("void xalm::gemv_kernel<%d, 1, 3, xalm::GemvShape<512, 2, 4, true, 4, true, 2, 2> >"
+                               % w["wdt"])
+    roofline = {"bound": "hbm", "achieved": round(k_gbps, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                "frac": round(k_gbps / HBM_PEAK_GBPS, 4), "traffic": traffic,
+                "traffic_source": src,
+                "kernel": "gemv_kernel<PRO_RMSNORM,EPI_GLU> (fused W1/W3 + rmsnorm + silu*up), layers rotating",
+                "bytes_per_launch": k_bytes, "avg_launch_us": round(k_us, 2)}
     value = job_value(world, args.steps, elapsed)
     if rank == 0:
         out = {
@@ -355,10 +408,8 @@ def main():
             "data": "synthetic (deterministic xalm_synth weights of the named shapes; no checkpoint offline)",
             "config": {"workload": w["desc"], "prompt_tokens": len(prompt), "max_seq_len": c.max_seq_len,
                        "kv_len_timed": [pos + 1, pos + args.steps], "batch": 1, "parallelism": f"replicas x{world}",
-                       "engine": "persistent" if engine == 1 else "stream (LDS-DMA weight ring)" if engine == 2 else
-                       {2: "graph, qkv+attention+Wo fused", 1: "graph, attention+Wo fused",
-                        0: "graph"}[model.get_option(L.OPT_FUSE_ATTN_WO)] +
-                       (f", column attention+Wo for kv_len <= {col_max}" if col_max else "")},
+                       "engine": {1: "hipGraph per token, attention+Wo fused",
+                                  0: "hipGraph per token"}[model.get_option(L.OPT_FUSE_ATTN_WO)]},
             "roofline": roofline,
             "hbm_step": {"achieved_GBps": round(step_gbps, 1), "frac": round(step_gbps / HBM_PEAK_GBPS, 4),
                          "bytes_per_token": step_bytes // args.steps,

@@ -39,7 +39,7 @@ enum xh_dtype {
     XH_U8 = 8,
     XH_Q8 = 9, /* int8 * 0.01f, src/types.h:423-424 */
     /* The converter's gguf blocks (convert.py:176-187 `--type q8_0 / q4_0`, quants.py): 32
-     * elements per block, an f16 scale d first.  Q8_0 (quants.py:438-454): 34 B = d + 32
+     * elements per block, an f16 scale d first.  Q8_0 (quants.py:441-463): 34 B = d + 32
      * int8, value d*q.  Q4_0 (quants.py:281-311): 18 B = d + 16 bytes, byte j holding element
      * j (low nibble) and j+16 (high nibble), value d*(nibble-8).  Tensors are uploaded in that
      * file layout ([rows][cols/32 blocks], header shape = bytes per row); the reference C++
@@ -48,7 +48,7 @@ enum xh_dtype {
     XH_Q4_0 = 21
 };
 
-/* ---- tensor kinds (names as in .xalm, src/model.cpp:399-430) ----------------------- */
+/* ---- tensor kinds (names as in .xalm, src/model.cpp:83-114) ------------------------ */
 enum xh_tensor_kind {
     XH_EMBED = 0,      /* embed.weight          [vocab, dim]              */
     XH_ATTN_NORM = 1,  /* l.N.attn.norm.weight  [dim]                     */
@@ -106,7 +106,7 @@ const char* xh_last_error(const xh_ctx* ctx); /* ctx may be NULL: last create er
 
 /* Copy one host tensor (`bytes` must equal shape*elem size) to the device.  `layer` is
  * ignored for embed/final_norm/wcls.  Shape and dtype are validated against the config
- * (mirrors the load_tensor checks, src/model.cpp:378-397).  Matrices of one layer that
+ * (mirrors the load_tensor checks, src/model.cpp:62-81).  Matrices of one layer that
  * the kernels fuse (q/k/v, gate/up) must share one dtype. */
 int xh_upload(xh_ctx* ctx, int tensor_kind, int layer, int dtype, const void* host, size_t bytes);
 
@@ -153,31 +153,10 @@ int xh_prefill(xh_ctx* ctx, const int* tokens, int n, int pos0, int want_logits,
  * reference does in double. */
 int xh_perplexity(xh_ctx* ctx, const int* tokens, int n, int pos0, float* probs_out);
 
-/* Device engine: 0 = one hipGraph of kernels per token (gemv / attention launches);
- * 1 = the persistent decode kernel (one launch per call, every phase inside, weights
- * prefetched into registers across the hand-offs); 2 = the stream kernel (one launch per
- * call; one loader wave per CU streams every weight row through an LDS-DMA ring ahead of the
- * hand-offs, consumer waves compute from the ring).  1 and 2 need one dtype for all layer
- * matrices and norms and an instantiated head shape; 2 also rows of whole 1 KiB (f16: dim,
- * q_dim and hidden multiples of 512).  -1 = automatic (currently the graph engine).  All
- * compute the same math (reduction orders differ, within the tolerances); xh_set_engine
- * returns XH_E_INVALID for an engine that cannot run these weights. */
-int xh_set_engine(xh_ctx* ctx, int engine);
-int xh_get_engine(const xh_ctx* ctx); /* the engine the next call will use */
-/* Device time (HIP events on the context's stream) of the last persistent-engine launch,
- * in microseconds: one launch covers a whole xh_prefill / xh_decode_greedy call. */
-int xh_last_launch_us(const xh_ctx* ctx, float* us);
-/* Debug timelines.  enable (bits): 1 = persistent engine, 2 = fused attention + Wo launches,
- * 4 = fused qkv + attention + Wo launches ([workgroup][8] stamps, see qaw.h)
- * ([workgroup][4] stamps: start, attention done / hand-off passed, end; each launch
- * overwrites), 0 = off, -1 = unchanged.  Copies min(cap, *len) words of the last traced launch
- * to `out` first.  Persistent engine: for the launch's last token, workgroups {0, n_cu/2, n_cu-1} x [n_layers + 1][5 phases][2] device
- * clock stamps (100 MHz; 0 = not reached) — [l][p][0] hand-off passed, [l][p][1] published —
- * plus 2 words ([n_layers][1][1] = token start, [n_layers][1][0] = next token known).
- * 8 = stream engine: [n_cu][4] device-clock sums (loader waiting for a free ring slot,
- * consumer wave 0 waiting for a full slot, its hand-off waits, its attention), then for the
- * last token of CUs {0, n_cu/2, n_cu-1} [4 n_layers + 1 phases][4] stamps: input wait start,
- * input ready, matrix done, first slot issued by the loader. */
+/* Debug timeline of the fused attention + Wo launches.  enable: 2 = on (every attn_wo launch
+ * writes [workgroup][8] device-clock stamps, 100 MHz: start, attention done / hand-off passed,
+ * end, split known, scores done, p.V done, partial drained; each launch overwrites), 0 = off,
+ * -1 = unchanged.  Copies min(cap, *len) words of the last traced launch to `out` first. */
 int xh_debug_trace(xh_ctx* ctx, int enable, uint64_t* out, int cap, int* len);
 
 /* Copy the current device logits to the host. */
@@ -197,10 +176,8 @@ size_t xh_active_bytes(const xh_ctx* ctx, size_t pos);
 /* Graph capture of the per-token step (default on).  Off = eager launches (debugging). */
 int xh_set_graphs(xh_ctx* ctx, int enable);
 
-/* Graph-engine variants.  XH_OPT_FUSE_ATTN_WO (default 1): 2 = rmsnorm + Wq/Wk/Wv, attention
- * and Wo (+ residual) in ONE launch with in-launch hand-offs (qaw.h); 1 = qkv launch, then
- * attention + Wo in one launch (attn_wo.h); 0 = three launches.  Same math.  Level 2 falls
- * back to 1 where the shape is not instantiated; xh_get_option reports the level in effect. */
+/* Launch-structure variants.  XH_OPT_FUSE_ATTN_WO (default 1): 1 = attention and Wo (+ residual)
+ * in one launch with an in-launch hand-off (attn_wo.h); 0 = two launches.  Same math. */
 /* XH_OPT_PREFILL (default 1): xh_prefill / xh_perplexity process the prompt in passes of up to
  * 64 tokens, each weight matrix streamed once per pass into MFMA GEMMs (prefill.h): 1 = f32-input
  * MFMA (activations exactly as the reference), except fp8 weights, which take the split-f16
@@ -212,15 +189,7 @@ int xh_set_graphs(xh_ctx* ctx, int enable);
  * epilogue of the W1/W3 GEMM writes those f16 hi/lo fragments directly (one launch); 0 = GLU to
  * f32 first, then split in the W2 GEMM's input pass (two launches).  Bit-identical results; a
  * debug knob so tests cover both routes. */
-/* XH_OPT_COL_KV_MAX (default 0 = off, at most 256): at fusion level 1, decode steps whose
- * history (kv_len) is at most this take the column form of attention + Wo (attn_col.h): each
- * workgroup serves one KV head and a block of Wo rows, computes that head's attention itself and
- * multiplies it by its slice of Wo's columns; the W1/W3 launch's rmsnorm sums the per-head
- * partials.  No hand-off between workgroups; every workgroup of a head pulls that head's whole
- * K/V history into LDS (served by its XCD's L2), so longer histories keep the split-KV form.  xh_get_option reports 0 where the weights or the
- * head shape do not take it (f32 Wo beyond 64 chunks per head, exact fp8 decode, > 8 KV heads).
- * Measured no faster than the default form on MI355X; kept as an option. */
-enum xh_option { XH_OPT_FUSE_ATTN_WO = 1, XH_OPT_PREFILL = 2, XH_OPT_PREFILL_GLU_SPLIT = 3, XH_OPT_COL_KV_MAX = 4 };
+enum xh_option { XH_OPT_FUSE_ATTN_WO = 1, XH_OPT_PREFILL = 2, XH_OPT_PREFILL_GLU_SPLIT = 3 };
 int xh_set_option(xh_ctx* ctx, int option, int value);
 int xh_get_option(const xh_ctx* ctx, int option, int* value);
 
@@ -237,9 +206,9 @@ int xh_op_mha(float* xout, const uint16_t* kb, const uint16_t* vb, const float* 
 
 /* ---- timing hooks used by bench.py (HIP events on the context's own stream) -------- */
 /* Average device time (microseconds) of one launch of kernel `which` (0 = the fused
- * gate/up matvec of layer 0, 1 = qkv, 2 = wo, 3 = down, 4 = lm_head, 5 = attention, 6 = the
- * column-form attention + Wo, 7 = the gate/up matvec summing the column form's partials)
- * over `iters` back-to-back launches with the current step parameters. */
+ * gate/up matvec, 1 = qkv, 2 = wo, 3 = down, 4 = lm_head, 5 = attention) over `iters`
+ * back-to-back launches with the current step parameters (layers rotate, so the Infinity Cache
+ * never serves a repeat). */
 int xh_time_kernel(xh_ctx* ctx, int which, int iters, float* avg_us);
 /* Bytes one launch of that kernel must move (algorithmic). */
 size_t xh_kernel_bytes(const xh_ctx* ctx, int which, int kv_len);

@@ -41,6 +41,7 @@ def _load():
             "xo_f16_to_f32": (ctypes.c_float, [ctypes.c_uint16]),
             "xo_sample_argmax": (_I, [_P, _I]), "xo_sample_prob": (ctypes.c_float, [_P, _I, _I]),
             "xo_num_threads": (_I, []), "xo_set_threads": (None, [_I]),
+            "xo_set_matmul_order": (None, [_I]), "xo_matmul_order": (_I, []),
             "xo_fill_synthetic": (None, [_P, _SZ, _SZ, _I, ctypes.c_uint64, ctypes.c_float, ctypes.c_float]),
         }
         for name, (res, args) in sig.items():
@@ -199,6 +200,17 @@ def num_threads():
 
 def set_threads(n):
     _load().xo_set_threads(int(n))
+
+
+def set_matmul_order(order):
+    """f16 matmul in-row order: 0 = 8-wide FMA lanes (default), 1 = sequential.  Both read the
+    reference's `omp simd` row loop (src/infer.cpp:104-135) validly; their difference is the
+    reference algorithm's own rounding-order sensitivity."""
+    _load().xo_set_matmul_order(int(order))
+
+
+def matmul_order():
+    return int(_load().xo_matmul_order())
 
 
 _NP = {1: np.float32, 2: np.uint16, 3: np.uint16, 6: np.uint8, 7: np.uint8, 20: np.uint8, 21: np.uint8}

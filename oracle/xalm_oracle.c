@@ -164,10 +164,18 @@ static size_t dtype_bits(int dtype) {
 /* matmul<TX,TW>, src/infer.cpp:104-135 (dispatch :185-216): xout[i] = sum_j dec(W[i,j])*x[j],
  * fp32 accumulate, OpenMP over rows (the reference's `omp simd` leaves the in-row order
  * implementation-defined; here 8-wide FMA lanes for f16). */
+/* in-row summation order of the f16 matmul: 0 = 8-wide FMA lanes (default), 1 = sequential
+ * (XO_MATMUL_SCALAR=1 or xo_set_matmul_order(1)); both are valid readings of the reference's
+ * `omp simd` loop, so their difference measures the reference's own order sensitivity */
+static int scalar_order = -1;
+void xo_set_matmul_order(int order) { scalar_order = order != 0; }
+int xo_matmul_order(void) {
+    if (scalar_order < 0) scalar_order = getenv("XO_MATMUL_SCALAR") && atoi(getenv("XO_MATMUL_SCALAR"));
+    return scalar_order;
+}
 void xo_matmul(float* xout, const float* x, const void* w, const int dtype, const int n, const int d) {
     int i;
-    static int scalar_order = -1; /* XO_MATMUL_SCALAR=1: sequential in-row order (sensitivity checks) */
-    if (scalar_order < 0) scalar_order = getenv("XO_MATMUL_SCALAR") && atoi(getenv("XO_MATMUL_SCALAR"));
+    if (scalar_order < 0) xo_matmul_order();
     if (dtype == XH_F16 && !scalar_order) {
         const uint16_t* W = (const uint16_t*)w;
 #pragma omp parallel for schedule(static)

@@ -20,23 +20,15 @@ FIXTURES = ["tiny_mistral_f16", "tiny_mistral_bf16", "tiny_mistral_f32", "tiny_m
             "tiny_mistral_f8_e5m2", "small_llama_f16"]
 
 
-# "graph_qaw": hipGraph of kernels per token with rmsnorm + qkv, attention and Wo in ONE launch
-# (qaw.h, the default); "graph": qkv, then attention + Wo in one launch; "graph_split": three
-# launches; "persistent": one persistent kernel per call (xh_set_engine(1))
-# "graph_col": the graph with the column-form attention + Wo (attn_col.h, XH_OPT_COL_KV_MAX)
-ENGINES = ["graph_qaw", "graph", "graph_split", "graph_col", "persistent"]
-FUSE = {"graph_qaw": 2, "graph": 1, "graph_split": 0, "graph_col": 1, "persistent": 1}
+# launch structures of the hipGraph step: "graph": qkv, then attention + Wo in one launch
+# (attn_wo.h, the default); "graph_split": attention and Wo as two launches
+ENGINES = ["graph", "graph_split"]
+FUSE = {"graph": 1, "graph_split": 0}
 
 
 def configure(gm, engine):
-    gm.set_engine(1 if engine == "persistent" else 0)
     gm.set_option(L.OPT_FUSE_ATTN_WO, FUSE[engine])
-    if engine == "graph_col":
-        gm.set_option(L.OPT_COL_KV_MAX, 256)
-    assert gm.engine == (1 if engine == "persistent" else 0)
-    if engine != "persistent":
-        # the level in effect: every fixture's head shape is instantiated
-        assert gm.get_option(L.OPT_FUSE_ATTN_WO) == FUSE[engine]
+    assert gm.get_option(L.OPT_FUSE_ATTN_WO) == FUSE[engine]
 
 
 def tol(ref):
@@ -129,8 +121,8 @@ def test_hydrate_mode_then_logits(engine):
 @pytest.mark.parametrize("name,context", [("tiny_mistral_f16", 16), ("small_llama_f16", 0),
                                           ("tiny_mistral_f8_e4m3", 0)])
 def test_prefill_matches_oracle(name, context, engine):
-    # xh_prefill = the prompt loop of run_completion in one call (one launch on the persistent
-    # engine); KV rings and the last logits equal the oracle's token-by-token forward
+    # xh_prefill = the prompt loop of run_completion in one call; KV rings and the last logits
+    # equal the oracle's token-by-token forward
     xf = XalmFile(fixture_path(name + ".xalm"))
     gm = Model.from_xalm(xf, context=context)
     configure(gm, engine)
@@ -295,9 +287,8 @@ def test_batched_prefill_equals_token_loop(batched):
 
 
 def test_engines_agree_on_long_decode():
-    # 200 greedy tokens on the head_dim-128 fixture: the persistent engine's tokens equal the
-    # graph engine's (same per-row math; only the rmsnorm reduction order differs), logits
-    # within the tolerance after every step of a teacher-forced replay
+    # 120 greedy tokens on the head_dim-128 fixture: both launch structures give the same tokens
+    # (same per-row math) and logits within the tolerance
     xf = XalmFile(fixture_path("small_llama_f16.xalm"))
     res = []
     for engine in ENGINES:
@@ -413,14 +404,11 @@ def test_perplexity_probs_match_oracle(name, prefill):
     check_probs(gm.token_probs(toks), om, toks)
 
 
-@pytest.mark.parametrize("case", ["persistent", "ring"])
-def test_perplexity_token_loop_paths(case):
-    # the persistent engine, and a sequence longer than -T (ring wrap + sinks): token by token
+def test_perplexity_token_loop_ring():
+    # a sequence longer than -T (ring wrap + sinks): the token loop
     xf = XalmFile(fixture_path("tiny_mistral_f16.xalm"))
-    ctxlen = 16 if case == "ring" else 0
+    ctxlen = 16
     gm = Model.from_xalm(xf, context=ctxlen)
-    if case == "persistent":
-        gm.set_engine(1)
     om = O.OracleModel.from_xalm(xf, context=ctxlen)
     toks = [1] + [3 + (i * 23) % 290 for i in range(40)]
     check_probs(gm.token_probs(toks), om, toks)
@@ -550,8 +538,6 @@ def test_long_context_streaming_attention(engine, history):
     pos = history vs the oracle on the same weights and the same KV rows."""
     import bench
 
-    if engine == "persistent":
-        pytest.skip("the persistent engine's attention tiles do not fit a 32k split (graph engine only)")
     w = dict(dim=512, hidden=512, layers=2, heads=32, kv_heads=8, head_dim=128, vocab=256, msl=32768, theta=1e6,
              wdt=L.F16, edt=L.F16, cdt=L.F16)
     c = bench.make_config(w)

@@ -52,14 +52,11 @@ def test_matmul_blocks(dtype, n, d):
 @pytest.mark.parametrize("name", ["tiny_mistral_q8_0", "tiny_mistral_q4_0", "small_llama_q8_0"])
 @pytest.mark.parametrize("fuse", [1, 0])
 def test_forward_on_converter_blocks(name, fuse):
-    # every fixture position with logits vs the oracle; the graph engine (the one-launch
-    # engines and the MFMA prefill do not take block formats: graph + token loop)
+    # every fixture position with logits vs the oracle (the MFMA prefill does not take block
+    # formats: the token loop)
     xf = XalmFile(fixture_path(name + ".xalm"))
     gm = Model.from_xalm(xf)
     gm.set_option(L.OPT_FUSE_ATTN_WO, fuse)
-    with pytest.raises(L.XhError):  # the one-launch engines decline block formats
-        gm.set_engine(1)
-    assert gm.engine == 0
     om = O.OracleModel.from_xalm(xf)
     st = InferenceState(gm.config)
     toks = [1] + [3 + (i * 37) % (gm.config.vocab_size - 3) for i in range(20)]

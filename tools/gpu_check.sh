@@ -23,7 +23,6 @@ for s in $STEPS; do
         tests) run pytest_gpu 900 python -m pytest tests -m gpu -q --timeout 300 -rf ;;
         bench) run bench 600 python bench.py ;;
         bench_split) run bench_split 600 python bench.py --fuse-attn-wo 0 ;;
-        bench_pk) run bench_pk 600 python bench.py --engine 1 ;;
         bench_f8) run bench_f8 600 python bench.py --workload mistral-7b-f8 ;;
         bench_32k) run bench_32k 600 python bench.py --workload mistral-7b-f16-32k --steps 64 ;;
         bench_llama) run bench_llama 600 python bench.py --workload llama3-8b-f16 ;;

@@ -31,7 +31,6 @@ def row_bytes(dtype: int, n: int) -> int:
 OPT_FUSE_ATTN_WO = 1
 OPT_PREFILL = 2
 OPT_PREFILL_GLU_SPLIT = 3
-OPT_COL_KV_MAX = 4
 
 # enum xh_tensor_kind
 EMBED, ATTN_NORM, FFN_NORM, WQ, WK, WV, WO, W1, W2, W3, FINAL_NORM, WCLS = range(12)
@@ -71,9 +70,6 @@ _SIGNATURES = {
     "xh_decode_greedy": (_I, [_P, _I, _I, _I, _I, _P, ctypes.POINTER(_I)]),
     "xh_prefill": (_I, [_P, _P, _I, _I, _I, _P]),
     "xh_perplexity": (_I, [_P, _P, _I, _I, _P]),
-    "xh_set_engine": (_I, [_P, _I]),
-    "xh_get_engine": (_I, [_P]),
-    "xh_last_launch_us": (_I, [_P, _FP]),
     "xh_debug_trace": (_I, [_P, _I, _P, _I, ctypes.POINTER(_I)]),
     "xh_get_logits": (_I, [_P, _P]),
     "xh_reset": (_I, [_P]),

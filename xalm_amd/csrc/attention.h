@@ -75,17 +75,12 @@ struct AddArrive {
 // One workgroup of THREADS threads: KV head g, split s.  PARTIALS (attn_wo.h): every active
 // split stores its partial (o, m, l) write-through, drains, and adds 1 to *done; the
 // consumers merge (no ticket, no merge round trips inside the attention chain).
-// FUSED (qaw.h): q and this token's K/V row are produced inside the same launch.  The first
-// round of K/V rows is requested before `wait()` returns, except the rows this launch writes
-// (slot kv_pos, and the sink rows 0..kv_sink-1 that the qkv phase re-rotates): those, and q,
-// are read after the hand-off with sc1 loads only, so no stale copy of them can sit in this
-// CU's caches (MI355X_MICROARCH.md "Valid forms", consumer condition 1).
 // MINT: split floor (0 = the default of the mode); `arrive(done)` runs on thread 0.
 // SIGNAL (with !PARTIALS, attn_wo.h long contexts): the block that completes a KV head (its only
 // split, or the last split to arrive, which merges) stores the head's output write-through,
 // drains and calls arrive(done): the consumer waits for n_kv_heads arrivals and reads the
 // merged output, instead of merging n_active partials itself.
-template <int HD, int QPK, int THREADS, bool PARTIALS, bool FUSED = false, int MINT = 0, class Wait = NoWait,
+template <int HD, int QPK, int THREADS, bool PARTIALS, int MINT = 0, class Wait = NoWait,
           class Arrive = AddArrive, bool SIGNAL = false>
 __device__ __forceinline__ void attn_block(const AttnArgs& a, const int g, const int s, char* smem, unsigned* done,
                                            unsigned long long* dbg = nullptr, const Wait& wait = Wait(),
@@ -113,14 +108,8 @@ __device__ __forceinline__ void attn_block(const AttnArgs& a, const int g, const
     const int sub = tid % LPR, rr = tid / LPR;
     const float scale = 1.0f / sqrtf((float)HD);  // src/infer.cpp:338
     const size_t col = (size_t)g * HD + sub * 8;
-    // FUSED: rows written in this launch
-    const int kv_pos = FUSED ? a.sp->kv_pos : -1;
-    const int kv_sink = FUSED ? a.sp->kv_sink : 0;
-    auto fresh = [&](const int t) { return FUSED && (t == kv_pos || t < kv_sink); };
     auto ld_kv = [&](const uint16_t* base, const int t) {
-        const size_t off = ((size_t)t * a.kv_dim + col) * 2;
-        if (fresh(t)) return ld_sc1_x4(base, (uint32_t)off);
-        return *(const u32x4*)((const char*)base + off);
+        return *(const u32x4*)((const char*)base + ((size_t)t * a.kv_dim + col) * 2);
     };
 
     // ---- first round of K and V rows, requested before anything else ----
@@ -128,36 +117,18 @@ __device__ __forceinline__ void attn_block(const AttnArgs& a, const int g, const
 #pragma unroll
     for (int p = 0; p < ATTN_PREF; p++) {
         const int t = t0 + rr + p * RPP;
-        if (t < t1 && !fresh(t)) {
+        if (t < t1) {
             kr[p] = *(const u32x4*)(a.kc + (size_t)t * a.kv_dim + col);
             vr[p] = *(const u32x4*)(a.vc + (size_t)t * a.kv_dim + col);
         }
     }
+    wait();
     float qv[QPK][8];
-    if (FUSED) {
-        wait();
-#pragma unroll
-        for (int p = 0; p < ATTN_PREF; p++) {
-            const int t = t0 + rr + p * RPP;
-            if (t < t1 && fresh(t)) {
-                kr[p] = ld_kv(a.kc, t);
-                vr[p] = ld_kv(a.vc, t);
-            }
-        }
-    }
 #pragma unroll
     for (int h = 0; h < QPK; h++) {
         const size_t qo = (size_t)(g * QPK + h) * HD + sub * 8;
-        float4 q0, q1;
-        if (FUSED) {
-            const u32x4 u0 = ld_sc1_x4(a.q, (uint32_t)(qo * 4)), u1 = ld_sc1_x4(a.q, (uint32_t)(qo * 4 + 16));
-            q0 = make_float4(bits_f32(u0.x), bits_f32(u0.y), bits_f32(u0.z), bits_f32(u0.w));
-            q1 = make_float4(bits_f32(u1.x), bits_f32(u1.y), bits_f32(u1.z), bits_f32(u1.w));
-        } else {
-            const float4* qp = (const float4*)(a.q + qo);
-            q0 = qp[0];
-            q1 = qp[1];
-        }
+        const float4* qp = (const float4*)(a.q + qo);
+        const float4 q0 = qp[0], q1 = qp[1];
         qv[h][0] = q0.x; qv[h][1] = q0.y; qv[h][2] = q0.z; qv[h][3] = q0.w;
         qv[h][4] = q1.x; qv[h][5] = q1.y; qv[h][6] = q1.z; qv[h][7] = q1.w;
     }

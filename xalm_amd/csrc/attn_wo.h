@@ -62,7 +62,7 @@ __host__ __device__ constexpr size_t aw_image_bytes(const int n) {
 // x image of the Wo rows = the merged attention output.  Up to AW_MAXS partials (attn_wo.h: longer
 // histories arrive merged, aw_long) every thread loads its float4 of each partial AND its head's
 // (m, l) pairs in one round trip and forms the weights itself (n_active expf per thread): no LDS
-// exchange and no barrier between the loads and the image.  More partials (qaw.h): wts (LDS
+// exchange and no barrier between the loads and the image.  More partials: wts (LDS
 // [n_heads][n_active] weights, [n_heads] denominators, then the (m, l) pairs) shared per head.
 template <int E, int HD, int THREADS = AW_THREADS>
 __device__ __forceinline__ void aw_stage_merged(const AttnArgs& aa, const int n, const int n_active, float4* xs4,
@@ -199,10 +199,10 @@ __global__ __launch_bounds__(AW_THREADS) void attn_wo_kernel(const AttnArgs aa, 
         };
         if (merged) {
             // long contexts: each KV head's last split merges (ticket) and signals the head
-            attn_block<HD, QPK, AW_THREADS, false, false, attn_min_t_partials(HD, AW_THREADS), NoWait,
+            attn_block<HD, QPK, AW_THREADS, false, attn_min_t_partials(HD, AW_THREADS), NoWait,
                        decltype(arrive), true>(aa, g, s, smem, sync, nullptr, NoWait(), arrive);
         } else {
-            attn_block<HD, QPK, AW_THREADS, true, false, 0, NoWait, decltype(arrive)>(
+            attn_block<HD, QPK, AW_THREADS, true, 0, NoWait, decltype(arrive)>(
                 aa, g, s, smem, sync, trace ? trace + 8 * b : nullptr, NoWait(), arrive);
         }
         if (trace && threadIdx.x == 0) trace[8 * b + 1] = __builtin_amdgcn_s_memrealtime();

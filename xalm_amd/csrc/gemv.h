@@ -25,11 +25,7 @@
 
 namespace xalm {
 
-enum { PRO_PLAIN = 0, PRO_RMSNORM = 1, PRO_RMSNORM_P = 2 };
-// PRO_RMSNORM_P: x = x[0..n) + x[n..2n) + ... (np partial vectors, attn_col.h), summed in that
-// order, then rmsnorm as PRO_RMSNORM; workgroup 0 also stores the sum to x_out (the residual
-// stream the next EPI_RESID adds to)
-constexpr int PRO_PMAX = 8;
+enum { PRO_PLAIN = 0, PRO_RMSNORM = 1 };
 enum { EPI_STORE = 0, EPI_RESID = 1, EPI_QKV = 2, EPI_GLU = 3, EPI_LOGITS = 4 };
 
 constexpr int LDS_HEAD_BYTES = 64;  // block-reduction scratch in front of the x image
@@ -75,12 +71,10 @@ struct GemvArgs {
     unsigned long long* trace;  // debug (null = off): per workgroup [4] start, x staged, rows done
     unsigned long long* cand;   // EPI_LOGITS: [gridDim.x] argmax_key of the workgroup's best logit
     unsigned* aw_reset;         // workgroup 0 zeroes words 0, 32, ..., 256 (attn_wo.h sync of the layer)
-    int np;                     // PRO_RMSNORM_P: partial vectors at x (1 .. PRO_PMAX)
-    float* x_out;               // PRO_RMSNORM_P: [n] the summed x (workgroup 0)
 };
 
 // agent-scope relaxed (sc1: L1-bypassing, write-through) accesses for data handed between
-// kernels that run concurrently (chain.h)
+// workgroups of one launch
 __device__ __forceinline__ uint32_t ld_sc1_u32(const void* p) {
     return __hip_atomic_load((const uint32_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -158,48 +152,6 @@ __device__ __forceinline__ float4 load_norm4_nb(const void* w, const int dtype, 
 template <int E, int PRO, int THREADS, bool SC1 = false>
 __device__ __forceinline__ void stage_x(const GemvArgs& a, float4* xs4, float* red) {
     const int n = a.n;
-    auto slot = [&](const int i) {
-        const int c = i << 2;
-        const int it = c / (64 * E);
-        const int rem = c - it * 64 * E;
-        const int l = rem / E;
-        const int qd = (rem - l * E) >> 2;
-        return (it * (E / 4) + qd) * 64 + l;
-    };
-    if constexpr (PRO == PRO_RMSNORM_P) {
-        // pass 1: x = sum of the partials (fixed order) into the image, sum of squares as
-        // block_rms_scale; pass 2: scale * weight in place (same thread, same slots)
-        const float4* x4 = (const float4*)a.x;
-        const int n4 = n >> 2;
-        float ss = 0.f;
-        for (int i = threadIdx.x; i < n4; i += THREADS) {
-            float4 v = x4[i];
-            for (int k = 1; k < a.np; k++) {
-                const float4 p = x4[(size_t)k * n4 + i];
-                v.x += p.x; v.y += p.y; v.z += p.z; v.w += p.w;
-            }
-            ss += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
-            if (blockIdx.x == 0) ((float4*)a.x_out)[i] = v;
-            xs4[slot(i)] = v;
-        }
-        ss = wave_sum(ss);
-        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
-        __syncthreads();
-        float tot = 0.f;
-#pragma unroll
-        for (int w = 0; w < THREADS / 64; w++) tot += red[w];
-        const float scale = 1.0f / sqrtf(tot / (float)n + a.eps);
-        for (int i = threadIdx.x; i < n4; i += THREADS) {
-            float4 v = xs4[slot(i)];
-            const float4 w = load_norm4(a.norm_w, a.norm_dtype, i);
-            v.x = v.x * scale * w.x;  // x[i] * scale * weight[i], src/infer.cpp:234
-            v.y = v.y * scale * w.y;
-            v.z = v.z * scale * w.z;
-            v.w = v.w * scale * w.w;
-            xs4[slot(i)] = v;
-        }
-        return;
-    }
     float scale = 1.f;
     if (PRO == PRO_RMSNORM) scale = block_rms_scale<THREADS>(a.x, n, a.eps, red);
     const float4* x4 = (const float4*)a.x;
@@ -243,8 +195,8 @@ __device__ __forceinline__ void rotate_sinks(const GemvArgs& a, const int kv_sin
     }
 }
 
-// SC1: activations another in-flight kernel reads are stored write-through, and the residual
-// it may have written is read with sc1 loads (chain.h); otherwise plain accesses.
+// SC1: activations another workgroup of the same launch reads are stored write-through, and
+// the residual it may have written is read with sc1 loads; otherwise plain accesses.
 template <bool SC1>
 __device__ __forceinline__ void epi_st(float* p, const float v) {
     if (SC1) st_sc1_f(p, v);
@@ -650,18 +602,6 @@ __device__ __forceinline__ void stage_x_issue(const GemvArgs& a, float4 (&xv)[S:
     for (int j = 0; j < S::XN; j++) {
         const int i = min((int)threadIdx.x + j * S::THREADS, n4 - 1);
         xv[j] = x4[i];
-        if (PRO == PRO_RMSNORM_P) {
-            // partials 1 .. np-1 added in order; past np the last one is re-read and not added
-#pragma unroll
-            for (int k = 1; k < PRO_PMAX; k++) {
-                const float4 p = x4[(size_t)min(k, a.np - 1) * n4 + i];
-                const bool use = k < a.np;
-                xv[j].x += use ? p.x : 0.f;
-                xv[j].y += use ? p.y : 0.f;
-                xv[j].z += use ? p.z : 0.f;
-                xv[j].w += use ? p.w : 0.f;
-            }
-        }
         if (PRO != PRO_PLAIN) nw[j] = load_norm4_nb(a.norm_w, a.norm_dtype, a.n, i);
     }
 }
@@ -694,7 +634,6 @@ __device__ __forceinline__ void stage_x_finish(const GemvArgs& a, const float4 (
     for (int j = 0; j < S::XN; j++) {
         const int i = min((int)threadIdx.x + j * S::THREADS, n4 - 1);
         float4 v = xv[j];
-        if (PRO == PRO_RMSNORM_P && blockIdx.x == 0) ((float4*)a.x_out)[i] = v;
         if (PRO != PRO_PLAIN) {
             v.x = v.x * scale * nw[j].x;  // x[i] * scale * weight[i], src/infer.cpp:234
             v.y = v.y * scale * nw[j].y;

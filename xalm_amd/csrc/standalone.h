@@ -31,22 +31,20 @@ __global__ void rope_kernel(float* vec, int d, int head_dim, int pos, const floa
 }
 
 // Model::_copy_embedding (src/infer.cpp:553-602): x = dec(embed[token, :])
-// also advances the forward-step epoch of the fused launches' monotonic counters (qaw.h)
-__global__ void embed_kernel(const void* emb, int dtype, int dim, float* x, const StepParams* sp, unsigned* epoch) {
+__global__ void embed_kernel(const void* emb, int dtype, int dim, float* x, const StepParams* sp) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i == 0 && epoch) *epoch += 1;
     if (i < dim) x[i] = dec_row(dtype, emb, (size_t)sp->token, dim, i);
 }
 
 // Greedy decode step head: argmax over the lm_head workgroups' candidates (Sampler::
 // sample_argmax, src/sampler.cpp:19-30: the first maximum among logits > FLT_MIN, else token
 // 0), the decode-loop bookkeeping of argmax_advance (tokens[step], step, token, positions,
-// src/infer.cpp:611-613), the epoch, and x = embed[token] (Model::_copy_embedding,
+// src/infer.cpp:611-613) and x = embed[token] (Model::_copy_embedding,
 // src/infer.cpp:553-602), in one 1024-thread workgroup.
 constexpr int ARGMAX_CANDS = 1024;
 __global__ __launch_bounds__(1024) void argmax_embed_kernel(const unsigned long long* cand, StepParams* sp,
                                                             int* tokens, int cap, const void* emb, int dtype,
-                                                            int dim, float* x, unsigned* epoch) {
+                                                            int dim, float* x) {
     __shared__ unsigned long long kb[16];
     __shared__ int tok_s;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -68,7 +66,6 @@ __global__ __launch_bounds__(1024) void argmax_embed_kernel(const unsigned long 
         sp->token = tok;
         step_positions(sp, sp->pos_next);
         sp->pos_next += 1;
-        if (epoch) *epoch += 1;
         tok_s = tok;
     }
     __syncthreads();

@@ -5,7 +5,7 @@
 // ownership of Model::from_xalm (src/model.cpp:48-118).
 //
 // Per token the stream runs (all launches captured once into a hipGraph and replayed; the
-// token/position scalars live in device memory, StepParams). Default engine, fuse_level 1:
+// token/position scalars live in device memory, StepParams). Default, fuse level 1:
 //   embed_kernel (argmax_embed_kernel in the greedy graph)          x = embed[token]
 //   per layer:
 //     gemv<PRO_RMSNORM, EPI_QKV>    [Wq;Wk;Wv] (one fused matrix) + rmsnorm + clip + rope +
@@ -16,9 +16,10 @@
 //     gemv<PRO_PLAIN, EPI_RESID>    W2, x += .
 //   gemv<PRO_RMSNORM, EPI_STORE>    final rmsnorm + lm_head -> logits   (OUTPUT_LOGITS)
 //   gemv<PRO_RMSNORM, EPI_LOGITS>   ... + per-workgroup argmax candidates (greedy graph)
-// fuse_level 0 launches attention and Wo separately; 2 runs qkv + attention + Wo in one launch
-// (qaw.h); engine 1 is the persistent whole-token kernel (persistent.h). Prompts go through
-// prefill.h (passes of 64 tokens on f32 MFMA) unless XH_OPT_PREFILL is 0.
+// fuse_level 0 launches attention and Wo separately.  Prompts go through prefill.h (passes of
+// 64 tokens on MFMA) unless XH_OPT_PREFILL is 0.  (Round 2's one-launch engines — persistent,
+// LDS-DMA stream, qkv+attention+Wo, column-form attention — measured slower and were removed;
+// DESIGN.md §4.5 / §4.9 keep the measurements.)
 #include <hip/hip_runtime.h>
 #include <fcntl.h>
 #include <sys/mman.h>
@@ -41,7 +42,6 @@
 #include "gemv.h"
 #include "dt_launch.h"
 #include "prefill.h"
-#include "se_launch.h"
 #include "standalone.h"
 
 using namespace xalm;
@@ -115,11 +115,6 @@ struct xh_ctx {
     // fused attention + Wo launch (attn_wo.h): per-layer hand-off words [n_layers][4]
     bool fuse_attn_wo = true;
     unsigned* aw_sync = nullptr;
-    // qkv + attention + Wo in one launch (qaw.h), used when fuse_level == 2 and instantiated
-    int fuse_level = 1;  // 2 (qaw.h) measured slower end to end on MI355X: see DESIGN.md
-    unsigned* qaw_sync = nullptr;  // [n_layers][QAW_LAYER_WORDS] counters, then epoch, err
-    int qaw_nsplit = 1, qaw_t_max = 16;
-    bool qaw_ok = true;            // cleared when a launch reports the shape unsupported
     // batched prefill (prefill.h), buffers allocated on first use
     bool prefill_batched = true;
     // XH_OPT_PREFILL: 1 = split-f16 GEMMs for fp8 weights (measured faster), f32 MFMA otherwise;
@@ -146,60 +141,22 @@ struct xh_ctx {
     int ppl_cap = 0;
     int t_max_aw = 16;
     bool use_graphs = true;
-    // [0]: split-KV attention + Wo; [1]: the column form (attn_col.h) for histories <= col_kv_max
-    hipGraphExec_t g_logits[2] = {}, g_hydrate[2] = {}, g_decode[2] = {};
-    // column-form attention + Wo (attn_col.h): history bound (0 = off) and per-head partials
-    int col_kv_max = 0;
-    float* wo_part = nullptr;     // [n_kv_heads][dim]
-    unsigned* ac_err = nullptr;   // sticky device flag
+    hipGraphExec_t g_logits = nullptr, g_hydrate = nullptr, g_decode = nullptr;
     int max_gemv_waves = 4096;  // 16 waves per CU
     // the qkv launch: its whole matrix is one round at 16 waves per CU (every wave one group,
     // requested at once); at 8 waves per CU each wave streams two groups back to back
     // (tools/gemv_bench GB_T1K: 10.95 -> 10.12 us f16, 7.93 -> 7.34 us fp8)
     int qkv_waves = 2048;
-    // persistent engine (persistent.h)
-    int engine = -1;            // -1 auto, 0 graph of kernels, 1 persistent, 2 stream (stream.h)
     int n_cu = 0;
-    PkLayer* pk_layers = nullptr;        // device [n_layers]
-    unsigned* pk_counters = nullptr;     // device [n_layers * PK_PHASES + 1][PK_CSLOT] (sharded)
-    int* pk_tickets = nullptr;           // device [n_kv_heads]
-    int* pk_err = nullptr;               // device [2]: err, n_done
-    unsigned long long* pk_cand = nullptr;  // device [n_cu]
-    int* pk_prompt = nullptr;            // device [pk_prompt_cap]
-    int pk_prompt_cap = 0;
-    int* pk_host = nullptr;              // pinned [2 + pk_prompt_cap]: err, n_done, prompt staging
-    bool pk_layers_dirty = true;
-    hipEvent_t pk_ev[2] = {nullptr, nullptr};  // bracket every persistent launch
-    float pk_last_us = 0.f;
-    unsigned long long* pk_trace = nullptr;  // device [PK_TRACE_WG][pk_trace_len]
-    bool pk_trace_on = false;
-    bool aw_trace_on = false;  // fused attention + Wo launches write pk_trace (debug)
-    bool qaw_trace_on = false;  // fused qkv + attention + Wo launches write pk_trace (debug)
-    bool se_trace_on = false;   // stream kernel writes pk_trace (debug, stream.h SeArgs::trace)
-    // stream engine (stream.h): hand-off buffers, zeroed before every launch
-    SeLayer* se_layers = nullptr;            // device [n_layers]
-    unsigned long long* se_g = nullptr;      // device granules: x [dim], hb [hidden], attn [q_dim], cand [n_cu]
-    size_t se_g_words = 0;
-    unsigned* se_qcnt = nullptr;             // device [n_layers][n_kv_heads]
-    int* se_tickets = nullptr;               // device [n_kv_heads]
-    float *se_part_o = nullptr, *se_part_ml = nullptr;  // device [se_max_splits][n_heads][head_dim | 2]
-    int se_max_splits = 1;
-    int se_nslots = 0;                       // ring slots per CU (0: engine unavailable)
-    bool se_layers_dirty = true;
-
+    // attn_wo.h debug timeline (xh_debug_trace): [workgroup][8] device-clock stamps
+    unsigned long long* aw_trace = nullptr;
+    size_t aw_trace_len = 0;
+    bool aw_trace_on = false;
     uint16_t* kcache(int l) { return kv + (size_t)l * 2 * c.max_seq_len * kv_dim; }
     uint16_t* vcache(int l) { return kcache(l) + (size_t)c.max_seq_len * kv_dim; }
 };
 
 namespace {
-
-constexpr int QAW_LAYER_WORDS = (2 * CHAIN_SHARDS + 1) * CHAIN_SHARD_STRIDE;
-// XH_OPT_COL_KV_MAX default: histories up to this many slots take the column form (attn_col.h).
-// Off: measured no faster than the split-KV attention + Wo launch on MI355X
-constexpr int XH_COL_KV_MAX_DEFAULT = 0;
-unsigned* qaw_epoch(const xh_ctx* ctx) { return ctx->qaw_sync + (size_t)ctx->c.n_layers * QAW_LAYER_WORDS; }
-int* qaw_err(const xh_ctx* ctx) { return (int*)(qaw_epoch(ctx) + CHAIN_SHARD_STRIDE); }
-size_t qaw_words(const xh_config& c) { return (size_t)c.n_layers * QAW_LAYER_WORDS + 2 * CHAIN_SHARD_STRIDE; }
 
 int set_err(xh_ctx* ctx, int code, const char* fmt, ...) {
     char buf[1024];
@@ -408,13 +365,6 @@ GemvArgs w13_args(xh_ctx* ctx, int l) {
     a.out = ctx->hb; a.act = ctx->c.act; a.sp = ctx->sp;
     return a;
 }
-// W1/W3 after the column form: x = the sum of the n_kv_heads Wo partials (head 0 holds the
-// residual), stored back to ctx->x by workgroup 0 for W2's residual add
-GemvArgs w13_col_args(xh_ctx* ctx, int l) {
-    GemvArgs a = w13_args(ctx, l);
-    a.x = ctx->wo_part; a.np = ctx->c.n_kv_heads; a.x_out = ctx->x;
-    return a;
-}
 GemvArgs w2_args(xh_ctx* ctx, int l) {
     const LayerW& w = ctx->L[l];
     GemvArgs a{};
@@ -489,152 +439,59 @@ int launch_attn_wo(xh_ctx* ctx, int l, hipStream_t s) {
     const int hd = ctx->c.head_dim, qpk = ctx->qpk, nkv = ctx->c.n_kv_heads, tm = ctx->t_max_aw;
     const int mw = ctx->max_gemv_waves;
     switch (ctx->L[l].wo_dt) {
-        case XH_F32: return aw_launch_dt1(aa, ga, hd, qpk, nkv, tm, sync, mw, s, ctx->aw_trace_on ? ctx->pk_trace : nullptr);
-        case XH_F16: return aw_launch_dt2(aa, ga, hd, qpk, nkv, tm, sync, mw, s, ctx->aw_trace_on ? ctx->pk_trace : nullptr);
-        case XH_BF16: return aw_launch_dt3(aa, ga, hd, qpk, nkv, tm, sync, mw, s, ctx->aw_trace_on ? ctx->pk_trace : nullptr);
-        case XH_F8_E4M3: return aw_launch_dt6(aa, ga, hd, qpk, nkv, tm, sync, mw, s, ctx->aw_trace_on ? ctx->pk_trace : nullptr);
-        case XH_F8_E5M2: return aw_launch_dt7(aa, ga, hd, qpk, nkv, tm, sync, mw, s, ctx->aw_trace_on ? ctx->pk_trace : nullptr);
-        case XH_Q8: return aw_launch_dt9(aa, ga, hd, qpk, nkv, tm, sync, mw, s, ctx->aw_trace_on ? ctx->pk_trace : nullptr);
-        default: return XH_E_INVALID;
-    }
-}
-
-// column-form attention + Wo (attn_col.h): every layer's Wo takes it (dtype with a whole
-// power-of-two number of 16-B chunks per head slice, no exact-fp8 decode), <= AC_PMAX KV heads,
-// the graph engine with the attention + Wo fusion (level 1), a history within col_kv_max
-bool col_supported(const xh_ctx* ctx) {
-    const xh_config& c = ctx->c;
-    if (!ctx->wo_part || ctx->fuse_level != 1 || !ctx->fuse_attn_wo || c.n_kv_heads > AC_PMAX) return false;
-    if (c.dim % 4) return false;
-    for (const LayerW& w : ctx->L) {
-        if (w.wo_x) return false;
-        const int dt = w.wo_dt;
-        if (!(dt == XH_F32 || dt == XH_F16 || dt == XH_BF16 || dt == XH_F8_E4M3 || dt == XH_F8_E5M2 || dt == XH_Q8))
-            return false;
-        if (!acol_rows_per_wave(dt, c.head_dim, ctx->qpk)) return false;
-    }
-    return true;
-}
-bool use_col(const xh_ctx* ctx, int kv_len) {
-    return ctx->col_kv_max > 0 && kv_len <= std::min(ctx->col_kv_max, AC_KV_MAX) && col_supported(ctx);
-}
-int launch_attn_col(xh_ctx* ctx, int l, hipStream_t s) {
-    const LayerW& w = ctx->L[l];
-    const AttnArgs aa = attn_args(ctx, l);
-    AcArgs ac{};
-    ac.wo = w.wo; ac.row_bytes = (size_t)ctx->q_dim * dtype_size(w.wo_dt); ac.dim = ctx->c.dim;
-    ac.rows_per_wave = acol_rows_per_wave(w.wo_dt, ctx->c.head_dim, ctx->qpk);
-    ac.n_kv_heads = ctx->c.n_kv_heads; ac.x = ctx->x; ac.part = ctx->wo_part; ac.err = ctx->ac_err;
-    static const int ac_debug = getenv("XALM_AC_DEBUG") ? atoi(getenv("XALM_AC_DEBUG")) : 0;
-    ac.debug = ac_debug;
-    const int hd = ctx->c.head_dim, qpk = ctx->qpk;
-    switch (w.wo_dt) {
-        case XH_F32: return acol_launch_dt1(aa, ac, hd, qpk, s);
-        case XH_F16: return acol_launch_dt2(aa, ac, hd, qpk, s);
-        case XH_BF16: return acol_launch_dt3(aa, ac, hd, qpk, s);
-        case XH_F8_E4M3: return acol_launch_dt6(aa, ac, hd, qpk, s);
-        case XH_F8_E5M2: return acol_launch_dt7(aa, ac, hd, qpk, s);
-        case XH_Q8: return acol_launch_dt9(aa, ac, hd, qpk, s);
-        default: return XH_E_INVALID;
-    }
-}
-
-// qkv + attention + Wo launch of layer l; XH_E_INVALID = shape not instantiated (fall back)
-int launch_qaw(xh_ctx* ctx, int l, hipStream_t s) {
-    const LayerW& w = ctx->L[l];
-    if (w.qkv_dt != w.wo_dt || w.qkv_x || w.wo_x) return XH_E_INVALID;
-    AttnArgs aa = attn_args(ctx, l);
-    aa.nsplit = ctx->qaw_nsplit;
-    const GemvArgs qa = qkv_args(ctx, l), wa = wo_args(ctx, l);
-    QawSync sy{};
-    sy.qkv = ctx->qaw_sync + (size_t)l * QAW_LAYER_WORDS;
-    sy.heads = sy.qkv + CHAIN_SHARDS * CHAIN_SHARD_STRIDE;
-    sy.epoch = qaw_epoch(ctx);
-    sy.err = qaw_err(ctx);
-    sy.trace = ctx->qaw_trace_on ? ctx->pk_trace : nullptr;
-    const int hd = ctx->c.head_dim, qpk = ctx->qpk, nkv = ctx->c.n_kv_heads, tm = ctx->qaw_t_max, ncu = ctx->n_cu;
-    switch (w.qkv_dt) {
-        case XH_F32: return qaw_launch_dt1(qa, aa, wa, hd, qpk, nkv, tm, ncu, sy, s);
-        case XH_F16: return qaw_launch_dt2(qa, aa, wa, hd, qpk, nkv, tm, ncu, sy, s);
-        case XH_BF16: return qaw_launch_dt3(qa, aa, wa, hd, qpk, nkv, tm, ncu, sy, s);
-        case XH_F8_E4M3: return qaw_launch_dt6(qa, aa, wa, hd, qpk, nkv, tm, ncu, sy, s);
-        case XH_F8_E5M2: return qaw_launch_dt7(qa, aa, wa, hd, qpk, nkv, tm, ncu, sy, s);
-        case XH_Q8: return qaw_launch_dt9(qa, aa, wa, hd, qpk, nkv, tm, ncu, sy, s);
+        case XH_F32: return aw_launch_dt1(aa, ga, hd, qpk, nkv, tm, sync, mw, s, ctx->aw_trace_on ? ctx->aw_trace : nullptr);
+        case XH_F16: return aw_launch_dt2(aa, ga, hd, qpk, nkv, tm, sync, mw, s, ctx->aw_trace_on ? ctx->aw_trace : nullptr);
+        case XH_BF16: return aw_launch_dt3(aa, ga, hd, qpk, nkv, tm, sync, mw, s, ctx->aw_trace_on ? ctx->aw_trace : nullptr);
+        case XH_F8_E4M3: return aw_launch_dt6(aa, ga, hd, qpk, nkv, tm, sync, mw, s, ctx->aw_trace_on ? ctx->aw_trace : nullptr);
+        case XH_F8_E5M2: return aw_launch_dt7(aa, ga, hd, qpk, nkv, tm, sync, mw, s, ctx->aw_trace_on ? ctx->aw_trace : nullptr);
+        case XH_Q8: return aw_launch_dt9(aa, ga, hd, qpk, nkv, tm, sync, mw, s, ctx->aw_trace_on ? ctx->aw_trace : nullptr);
         default: return XH_E_INVALID;
     }
 }
 
 // a fused hand-off that timed out leaves its sticky flag: report it (after the stream sync)
 int check_aw(xh_ctx* ctx) {
-    {
-        int e = 0;
-        HIP_TRY(ctx, copy_sync(ctx, &e, qaw_err(ctx), sizeof(int), hipMemcpyDeviceToHost));
-        if (e) return set_err(ctx, XH_E_HIP, "qkv -> attention -> Wo hand-off timed out");
-    }
-    {
-        unsigned e = 0;
-        HIP_TRY(ctx, copy_sync(ctx, &e, ctx->ac_err, sizeof(unsigned), hipMemcpyDeviceToHost));
-        if (e) return set_err(ctx, XH_E_HIP, "column attention launched beyond its history bound");
-    }
     if (!ctx->fuse_attn_wo) return 0;
     std::vector<unsigned> h((size_t)ctx->c.n_layers * AW_SYNC_WORDS);
     HIP_TRY(ctx, copy_sync(ctx, h.data(), ctx->aw_sync, h.size() * sizeof(unsigned), hipMemcpyDeviceToHost));
     for (int l = 0; l < ctx->c.n_layers; l++)
-        if (h[(size_t)AW_SYNC_WORDS * l + 2]) return set_err(ctx, XH_E_HIP, "layer %d: attention -> Wo hand-off timed out", l);
+        if (h[(size_t)AW_SYNC_WORDS * l + 2]) {
+            // reported once: the sticky words are cleared so the context can be reset and reused
+            HIP_TRY(ctx, fill_sync(ctx, ctx->aw_sync, 0, h.size() * sizeof(unsigned)));
+            return set_err(ctx, XH_E_HIP, "layer %d: attention -> Wo hand-off timed out", l);
+        }
     return 0;
 }
 
 // greedy: the token is the argmax of the previous step's logits (argmax_embed_kernel)
-int enqueue_step(xh_ctx* ctx, hipStream_t s, bool with_logits, bool greedy = false, bool col = false) {
+int enqueue_step(xh_ctx* ctx, hipStream_t s, bool with_logits, bool greedy = false) {
     const xh_config& c = ctx->c;
     const int mb = ctx->max_gemv_waves;
-    // the qaw counters expect one epoch per step that launches qaw in every layer
-    unsigned* epoch = ctx->fuse_level >= 2 && ctx->qaw_ok && aw_instantiated(c.head_dim, ctx->qpk) ? qaw_epoch(ctx)
-                                                                                                    : nullptr;
     if (greedy)
         hipLaunchKernelGGL(argmax_embed_kernel, dim3(1), dim3(ARGMAX_CANDS), 0, s, (const unsigned long long*)ctx->cand,
                            ctx->sp, ctx->dec_tokens, ctx->dec_cap, (const void*)ctx->embed, ctx->embed_dt, c.dim,
-                           ctx->x, epoch);
+                           ctx->x);
     else
         hipLaunchKernelGGL(embed_kernel, dim3((c.dim + 255) / 256), dim3(256), 0, s, (const void*)ctx->embed,
-                           ctx->embed_dt, c.dim, ctx->x, (const StepParams*)ctx->sp, epoch);
+                           ctx->embed_dt, c.dim, ctx->x, (const StepParams*)ctx->sp);
     for (int l = 0; l < c.n_layers; l++) {
         const LayerW& w = ctx->L[l];
-        if (ctx->fuse_level >= 2 && ctx->qaw_ok && aw_instantiated(c.head_dim, ctx->qpk)) {
-            const int rc = launch_qaw(ctx, l, s);
-            if (rc == 0) goto mlp;
-            if (rc != XH_E_INVALID) return set_err(ctx, rc, "layer %d: qkv + attention + Wo launch failed", l);
-            ctx->qaw_ok = false;  // not instantiated / does not fit: the two-launch form from now on
-        }
         if (!launch_gemv<PRO_RMSNORM, EPI_QKV>(kdt(w.qkv_dt, w.qkv_x), qkv_args(ctx, l), s, qkv_launch_waves(ctx, l)))
             return set_err(ctx, XH_E_INVALID, "layer %d: unsupported qkv dtype %d", l, w.qkv_dt);
-        if (col) {
-            // attention + Wo by columns (attn_col.h), W1/W3's rmsnorm sums the head partials
-            const int rc = launch_attn_col(ctx, l, s);
-            if (rc) return set_err(ctx, rc, "layer %d: column attention + Wo launch failed", l);
-            if (!launch_gemv<PRO_RMSNORM_P, EPI_GLU>(kdt(w.w13_dt, w.w13_x), w13_col_args(ctx, l), s, mb))
-                return set_err(ctx, XH_E_INVALID, "layer %d: unsupported w1/w3 dtype", l);
-            goto w2;
-        }
+        GemvArgs a13 = w13_args(ctx, l);
         if (use_attn_wo(ctx, l)) {
             const int rc = launch_attn_wo(ctx, l, s);
             if (rc) return set_err(ctx, rc, "layer %d: fused attention + Wo launch failed", l);
             // W1/W3 right behind it zeroes its hand-off words for the next step
-            GemvArgs a = w13_args(ctx, l);
-            a.aw_reset = ctx->aw_sync + (size_t)AW_SYNC_WORDS * l;
-            if (!launch_gemv<PRO_RMSNORM, EPI_GLU>(kdt(w.w13_dt, w.w13_x), a, s, mb))
-                return set_err(ctx, XH_E_INVALID, "layer %d: unsupported w1/w3 dtype", l);
-            goto w2;
+            a13.aw_reset = ctx->aw_sync + (size_t)AW_SYNC_WORDS * l;
         } else {
             if (!launch_attn(attn_args(ctx, l), c.head_dim, ctx->qpk, c.n_kv_heads, ctx->t_max, s))
                 return set_err(ctx, XH_E_INVALID, "unsupported head_dim %d / q-per-kv %d", c.head_dim, ctx->qpk);
             if (!launch_gemv<PRO_PLAIN, EPI_RESID>(kdt(w.wo_dt, w.wo_x), wo_args(ctx, l), s, mb))
                 return set_err(ctx, XH_E_INVALID, "layer %d: unsupported wo dtype", l);
         }
-    mlp:
-        if (!launch_gemv<PRO_RMSNORM, EPI_GLU>(kdt(w.w13_dt, w.w13_x), w13_args(ctx, l), s, mb))
+        if (!launch_gemv<PRO_RMSNORM, EPI_GLU>(kdt(w.w13_dt, w.w13_x), a13, s, mb))
             return set_err(ctx, XH_E_INVALID, "layer %d: unsupported w1/w3 dtype", l);
-    w2:
         if (!launch_gemv<PRO_PLAIN, EPI_RESID>(kdt(w.w2_dt, w.w2_x), w2_args(ctx, l), s, mb))
             return set_err(ctx, XH_E_INVALID, "layer %d: unsupported w2 dtype", l);
     }
@@ -661,249 +518,17 @@ int check_ready(xh_ctx* ctx) {
     return 0;
 }
 
-// ---------------------------------------------------------------------------------------
-// persistent engine
-// ---------------------------------------------------------------------------------------
-int pk_nsplit(const xh_ctx* ctx) {
-    int ns = ctx->n_cu / ctx->c.n_kv_heads;
-    if (ns > 128) ns = 128;
-    return ns < 1 ? 1 : ns;
-}
-
-// One dtype for every matrix and one for every norm (the one-launch engines' kernels are
-// instantiated per matrix dtype), no fp8 matrix that needs the exact bit decode, and an
-// lm_head dtype the instantiations cover (fp8 models: bf16 per convert.py, or fp8).
-bool uniform_dtypes(const xh_ctx* ctx, int* dt, int* dtc, int* norm_dt) {
-    if (ctx->wcls_x) return false;
-    for (const LayerW& w : ctx->L)
-        if (w.qkv_x || w.w13_x || w.wo_x || w.w2_x) return false;  // exact fp8 decode: graph engine
-    *dt = ctx->L[0].qkv_dt;
-    *norm_dt = ctx->L[0].an_dt;
-    for (const LayerW& w : ctx->L)
-        if (w.qkv_dt != *dt || w.wo_dt != *dt || w.w13_dt != *dt || w.w2_dt != *dt || w.an_dt != *norm_dt ||
-            w.fn_dt != *norm_dt)
-            return false;
-    if (ctx->final_norm_dt != *norm_dt) return false;
-    *dtc = ctx->wcls_dt;
-    switch (*dt) {
-        case XH_F16: return *dtc == XH_F16;
-        case XH_BF16: return *dtc == XH_BF16;
-        case XH_F32: return *dtc == XH_F32;
-        case XH_F8_E4M3: return *dtc == XH_BF16 || *dtc == XH_F8_E4M3;
-        case XH_F8_E5M2: return *dtc == XH_F8_E5M2 || *dtc == XH_BF16;
-        default: return false;
-    }
-}
-
-// the weight dtypes the persistent kernel is instantiated for, or false
-bool pk_dtypes(const xh_ctx* ctx, int* dt, int* dtc, int* norm_dt) {
-    if (!uniform_dtypes(ctx, dt, dtc, norm_dt)) return false;
-    // pk_stage holds at most 8 float4 of x per thread
-    if (ctx->c.hidden_dim > 32 * PK_THREADS || ctx->c.dim > 32 * PK_THREADS || ctx->q_dim > 32 * PK_THREADS) return false;
-    const xh_config& c = ctx->c;
-    return (c.head_dim == 128 && (ctx->qpk == 4 || ctx->qpk == 8)) || (c.head_dim == 16 && ctx->qpk == 2) ||
-           (c.head_dim == 64 && ctx->qpk == 4);
-}
-
-// automatic selection = the graph engine: measured faster on MI355X (3.0 vs 4.3 ms per
-// Mistral-7B token; the persistent kernel's one-counter hand-offs cost ~45 us per layer)
-bool se_supported(const xh_ctx* ctx, int* dt, int* dtc, int* norm_dt);
-// a one-launch engine (1: persistent.h, 2: stream.h) is selected and handles these weights
-bool use_persistent(xh_ctx* ctx) {
-    int dt, dtc, ndt;
-    if (ctx->engine == 2) return se_supported(ctx, &dt, &dtc, &ndt);
-    if (ctx->engine != 1) return false;
-    return pk_dtypes(ctx, &dt, &dtc, &ndt);
-}
-int run_stream(xh_ctx* ctx, const int* prompt, int n_prompt, int n_gen, int pos0, int logits_last, int stop_a,
-               int stop_b, int* n_done_out);
-
-// One persistent launch: n_prompt tokens from `prompt` (host), then n_gen greedy tokens.
-int run_persistent(xh_ctx* ctx, const int* prompt, int n_prompt, int n_gen, int pos0, int logits_last, int stop_a,
-                   int stop_b, int* n_done_out) {
-    if (ctx->engine == 2) return run_stream(ctx, prompt, n_prompt, n_gen, pos0, logits_last, stop_a, stop_b, n_done_out);
-    ctx->cand_valid = false;  // its logits come without lm_head candidates
-    const xh_config& c = ctx->c;
-    int dt, dtc, ndt;
-    if (!pk_dtypes(ctx, &dt, &dtc, &ndt))
-        return set_err(ctx, XH_E_INVALID, "persistent engine needs one dtype for all matrices and all norms");
-    if (n_prompt > ctx->pk_prompt_cap || n_gen > ctx->dec_cap) return set_err(ctx, XH_E_INVALID, "too many tokens");
-    if (ctx->pk_layers_dirty) {
-        std::vector<PkLayer> h(c.n_layers);
-        for (int l = 0; l < c.n_layers; l++) {
-            const LayerW& w = ctx->L[l];
-            h[l] = PkLayer{w.wqkv, w.wo, w.w13, w.w2, w.attn_norm, w.ffn_norm, ctx->kcache(l), ctx->vcache(l)};
-        }
-        HIP_TRY(ctx, copy_sync(ctx, ctx->pk_layers, h.data(), h.size() * sizeof(PkLayer), hipMemcpyHostToDevice));
-        ctx->pk_layers_dirty = false;
-    }
-    if (n_prompt) {
-        memcpy(ctx->pk_host + 2, prompt, (size_t)n_prompt * sizeof(int));
-        HIP_TRY(ctx, hipMemcpyAsync(ctx->pk_prompt, ctx->pk_host + 2, (size_t)n_prompt * sizeof(int),
-                                    hipMemcpyHostToDevice, ctx->stream));
-    }
-    HIP_TRY(ctx, hipMemsetAsync(ctx->pk_counters, 0, ((size_t)c.n_layers * PK_PHASES + 1) * PK_CSLOT * sizeof(unsigned),
-                                ctx->stream));
-    HIP_TRY(ctx, hipMemsetAsync(ctx->pk_err, 0, 2 * sizeof(int), ctx->stream));
-    PkArgs a{};
-    a.n_layers = c.n_layers; a.dim = c.dim; a.hidden = c.hidden_dim; a.q_dim = ctx->q_dim; a.kv_dim = ctx->kv_dim;
-    a.head_dim = c.head_dim; a.n_heads = c.n_heads; a.n_kv_heads = c.n_kv_heads; a.vocab = c.vocab_size;
-    a.max_seq_len = c.max_seq_len; a.eps = c.norm_eps; a.qkv_clip = c.qkv_clip; a.act = c.act; a.norm_dt = ndt;
-    a.embed = ctx->embed; a.embed_dt = ctx->embed_dt; a.final_norm = ctx->final_norm; a.wcls = ctx->wcls;
-    a.layers = ctx->pk_layers; a.rope_freq = ctx->rope_freq; a.sink_cos = ctx->sink_cos; a.sink_sin = ctx->sink_sin;
-    a.x = ctx->x; a.q = ctx->q; a.attn = ctx->attn_out; a.hb = ctx->hb; a.logits = ctx->logits;
-    a.part_o = ctx->part_o; a.part_ml = ctx->part_ml; a.cand = ctx->pk_cand; a.nsplit = pk_nsplit(ctx);
-    a.counters = ctx->pk_counters; a.tickets = ctx->pk_tickets; a.err = ctx->pk_err;
-    a.prompt = ctx->pk_prompt; a.n_prompt = n_prompt; a.n_gen = n_gen; a.pos0 = pos0; a.logits_last = logits_last;
-    a.stop_a = stop_a; a.stop_b = stop_b; a.tokens_out = ctx->dec_tokens; a.n_done = ctx->pk_err + 1;
-    a.trace = ctx->pk_trace_on ? ctx->pk_trace : nullptr;
-    char msg[256] = {0};
-    HIP_TRY(ctx, hipEventRecord(ctx->pk_ev[0], ctx->stream));
-    int rc;
-    switch (dt) {
-        case XH_F32: rc = pk_launch_dt1(a, dtc, ctx->n_cu, ctx->stream, msg, sizeof msg); break;
-        case XH_F16: rc = pk_launch_dt2(a, dtc, ctx->n_cu, ctx->stream, msg, sizeof msg); break;
-        case XH_BF16: rc = pk_launch_dt3(a, dtc, ctx->n_cu, ctx->stream, msg, sizeof msg); break;
-        case XH_F8_E4M3: rc = pk_launch_dt6(a, dtc, ctx->n_cu, ctx->stream, msg, sizeof msg); break;
-        case XH_F8_E5M2: rc = pk_launch_dt7(a, dtc, ctx->n_cu, ctx->stream, msg, sizeof msg); break;
-        default: rc = XH_E_INVALID; snprintf(msg, sizeof msg, "persistent engine: dtype %d", dt);
-    }
-    if (rc) return set_err(ctx, rc, "%s", msg);
-    HIP_TRY(ctx, hipEventRecord(ctx->pk_ev[1], ctx->stream));
-    HIP_TRY(ctx, hipMemcpyAsync(ctx->pk_host, ctx->pk_err, 2 * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
-    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-    float ms = 0.f;
-    HIP_TRY(ctx, hipEventElapsedTime(&ms, ctx->pk_ev[0], ctx->pk_ev[1]));
-    ctx->pk_last_us = ms * 1000.f;
-    if (ctx->pk_host[0]) return set_err(ctx, XH_E_HIP, "persistent kernel: a hand-off timed out (2 s)");
-    if (n_done_out) *n_done_out = ctx->pk_host[1];
-    return 0;
-}
-
-// ---------------------------------------------------------------------------------------
-// stream engine (stream.h)
-// ---------------------------------------------------------------------------------------
-// The weights and shapes the stream kernel handles: one dtype for every matrix and one for
-// every norm (as the persistent engine), rows of whole 1 KiB K-steps, each consumer wave's
-// activations within SE_XF registers, an instantiated head shape.  Else false (graph engine).
-bool se_supported(const xh_ctx* ctx, int* dt, int* dtc, int* norm_dt) {
-    int d, dc, nd;
-    if (!uniform_dtypes(ctx, &d, &dc, &nd)) return false;
-    const xh_config& c = ctx->c;
-    if (!se_instantiated(c.head_dim, ctx->qpk) || ctx->se_nslots < SE_DEPTH + 1) return false;
-    const int E = elems_per_16b(d), EC = elems_per_16b(dc);
-    auto fits = [](int n, int e) {  // whole K-steps, at most SE_XF / e of them per consumer wave
-        if (n % (64 * e)) return false;
-        const int nk = n / (64 * e);
-        return (nk + SE_NW - 1) / SE_NW <= SE_XF / e;
-    };
-    if (!fits(c.dim, E) || !fits(ctx->q_dim, E) || !fits(c.hidden_dim, E) || !fits(c.dim, EC)) return false;
-    if (2 * ((c.dim / 2 + ctx->n_cu - 1) / ctx->n_cu) > SE_OWN_MAX) return false;  // residual rows per CU
-    if (c.vocab_size > 0x1FFFF || c.n_kv_heads > ctx->n_cu) return false;
-    *dt = d;
-    *dtc = dc;
-    *norm_dt = nd;
-    return true;
-}
-
-// One stream launch: n_prompt tokens from `prompt` (host), then n_gen greedy tokens.
-int run_stream(xh_ctx* ctx, const int* prompt, int n_prompt, int n_gen, int pos0, int logits_last, int stop_a,
-               int stop_b, int* n_done_out) {
-    ctx->cand_valid = false;  // its logits come without lm_head candidates
-    const xh_config& c = ctx->c;
-    int dt, dtc, ndt;
-    if (!se_supported(ctx, &dt, &dtc, &ndt)) return set_err(ctx, XH_E_INVALID, "stream engine not available for these weights");
-    if (n_prompt > ctx->pk_prompt_cap || n_gen > ctx->dec_cap) return set_err(ctx, XH_E_INVALID, "too many tokens");
-    if (ctx->se_layers_dirty) {
-        std::vector<SeLayer> h(c.n_layers);
-        for (int l = 0; l < c.n_layers; l++) {
-            const LayerW& w = ctx->L[l];
-            h[l] = SeLayer{w.wqkv, w.wo, w.w13, w.w2, w.attn_norm, w.ffn_norm, ctx->kcache(l), ctx->vcache(l)};
-        }
-        HIP_TRY(ctx, copy_sync(ctx, ctx->se_layers, h.data(), h.size() * sizeof(SeLayer), hipMemcpyHostToDevice));
-        ctx->se_layers_dirty = false;
-    }
-    if (n_prompt) {
-        memcpy(ctx->pk_host + 2, prompt, (size_t)n_prompt * sizeof(int));
-        HIP_TRY(ctx, hipMemcpyAsync(ctx->pk_prompt, ctx->pk_host + 2, (size_t)n_prompt * sizeof(int),
-                                    hipMemcpyHostToDevice, ctx->stream));
-    }
-    // every granule tag, counter and ticket starts at 0 (MI355X_MICROARCH.md: re-initialise every call)
-    HIP_TRY(ctx, hipMemsetAsync(ctx->se_g, 0, ctx->se_g_words * sizeof(unsigned long long), ctx->stream));
-    HIP_TRY(ctx, hipMemsetAsync(ctx->se_qcnt, 0, (size_t)c.n_layers * c.n_kv_heads * sizeof(unsigned), ctx->stream));
-    HIP_TRY(ctx, hipMemsetAsync(ctx->se_tickets, 0, (size_t)c.n_kv_heads * sizeof(int), ctx->stream));
-    HIP_TRY(ctx, hipMemsetAsync(ctx->pk_err, 0, 8 * sizeof(int), ctx->stream));
-    SeArgs a{};
-    a.n_layers = c.n_layers; a.dim = c.dim; a.hidden = c.hidden_dim; a.q_dim = ctx->q_dim; a.kv_dim = ctx->kv_dim;
-    a.head_dim = c.head_dim; a.n_heads = c.n_heads; a.n_kv_heads = c.n_kv_heads; a.vocab = c.vocab_size;
-    a.max_seq_len = c.max_seq_len; a.eps = c.norm_eps; a.qkv_clip = c.qkv_clip; a.act = c.act; a.norm_dt = ndt;
-    a.embed = ctx->embed; a.embed_dt = ctx->embed_dt; a.final_norm = ctx->final_norm; a.wcls = ctx->wcls;
-    a.layers = ctx->se_layers; a.rope_freq = ctx->rope_freq; a.sink_cos = ctx->sink_cos; a.sink_sin = ctx->sink_sin;
-    a.xg = ctx->se_g;
-    a.hg = a.xg + c.dim;
-    a.ag = a.hg + c.hidden_dim;
-    a.cg = a.ag + ctx->q_dim;
-    a.q = ctx->q; a.qcnt = ctx->se_qcnt; a.part_o = ctx->se_part_o; a.part_ml = ctx->se_part_ml;
-    a.tickets = ctx->se_tickets; a.logits = ctx->logits;
-    a.nslots = ctx->se_nslots;
-    // one batch of K/V row groups per attention wave (stream.h se_attention: SE_NA waves x
-    // 64 / (head_dim / 8) rows x 4)
-    a.split_rows = SE_NA * (64 / (c.head_dim / 8)) * 4;
-    a.max_splits = ctx->se_max_splits;
-    {
-        const char* ev = getenv("XALM_SE_ROTATE");  // experiment switch (default on)
-        a.rotate = ev ? atoi(ev) : 1;
-        const char* dv = getenv("XALM_SE_DEBUG");   // experiments only: results invalid
-        a.debug = dv ? atoi(dv) : 0;
-    }
-    a.err = ctx->pk_err;
-    a.prompt = ctx->pk_prompt; a.n_prompt = n_prompt; a.n_gen = n_gen; a.pos0 = pos0; a.logits_last = logits_last;
-    a.stop_a = stop_a; a.stop_b = stop_b; a.tokens_out = ctx->dec_tokens; a.n_done = ctx->pk_err + 1;
-    a.trace = ctx->se_trace_on ? ctx->pk_trace : nullptr;
-    char msg[256] = {0};
-    HIP_TRY(ctx, hipEventRecord(ctx->pk_ev[0], ctx->stream));
-    int rc;
-    switch (dt) {
-        case XH_F32: rc = se_launch_dt1(a, dtc, ctx->n_cu, ctx->stream, msg, sizeof msg); break;
-        case XH_F16: rc = se_launch_dt2(a, dtc, ctx->n_cu, ctx->stream, msg, sizeof msg); break;
-        case XH_BF16: rc = se_launch_dt3(a, dtc, ctx->n_cu, ctx->stream, msg, sizeof msg); break;
-        case XH_F8_E4M3: rc = se_launch_dt6(a, dtc, ctx->n_cu, ctx->stream, msg, sizeof msg); break;
-        case XH_F8_E5M2: rc = se_launch_dt7(a, dtc, ctx->n_cu, ctx->stream, msg, sizeof msg); break;
-        default: rc = XH_E_INVALID; snprintf(msg, sizeof msg, "stream engine: dtype %d", dt);
-    }
-    if (rc) return set_err(ctx, rc, "%s", msg);
-    HIP_TRY(ctx, hipEventRecord(ctx->pk_ev[1], ctx->stream));
-    HIP_TRY(ctx, hipMemcpyAsync(ctx->pk_host, ctx->pk_err, 2 * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
-    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-    float ms = 0.f;
-    HIP_TRY(ctx, hipEventElapsedTime(&ms, ctx->pk_ev[0], ctx->pk_ev[1]));
-    ctx->pk_last_us = ms * 1000.f;
-    if (ctx->pk_host[0]) {
-        int info[4] = {0, 0, 0, 0};
-        copy_sync(ctx, info, ctx->pk_err + 2, sizeof info, hipMemcpyDeviceToHost);
-        return set_err(ctx, XH_E_HIP, "stream kernel: a wait timed out (2 s): code %d workgroup %d wave %d value %d",
-                       info[0], info[1], info[2], info[3]);
-    }
-    if (n_done_out) *n_done_out = ctx->pk_host[1];
-    return 0;
-}
-
 void drop_graphs(xh_ctx* ctx) {
-    ctx->pk_layers_dirty = true;
-    ctx->se_layers_dirty = true;
-    for (int k = 0; k < 2; k++) {
-        if (ctx->g_logits[k]) hipGraphExecDestroy(ctx->g_logits[k]);
-        if (ctx->g_hydrate[k]) hipGraphExecDestroy(ctx->g_hydrate[k]);
-        if (ctx->g_decode[k]) hipGraphExecDestroy(ctx->g_decode[k]);
-        ctx->g_logits[k] = ctx->g_hydrate[k] = ctx->g_decode[k] = nullptr;
-    }
+    if (ctx->g_logits) hipGraphExecDestroy(ctx->g_logits);
+    if (ctx->g_hydrate) hipGraphExecDestroy(ctx->g_hydrate);
+    if (ctx->g_decode) hipGraphExecDestroy(ctx->g_decode);
+    ctx->g_logits = ctx->g_hydrate = ctx->g_decode = nullptr;
 }
 
-int capture(xh_ctx* ctx, int kind, bool col, hipGraphExec_t* out) {
+int capture(xh_ctx* ctx, int kind, hipGraphExec_t* out) {
     hipGraph_t g = nullptr;
     HIP_TRY(ctx, hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal));
-    int rc = 0;
-    rc = enqueue_step(ctx, ctx->stream, kind != 1, kind == 2, col);
+    const int rc = enqueue_step(ctx, ctx->stream, kind != 1, kind == 2);
     hipError_t e = hipStreamEndCapture(ctx->stream, &g);
     if (rc) { if (g) hipGraphDestroy(g); return rc; }
     if (e != hipSuccess) return set_err(ctx, XH_E_HIP, "graph capture failed: %s", hipGetErrorString(e));
@@ -913,14 +538,21 @@ int capture(xh_ctx* ctx, int kind, bool col, hipGraphExec_t* out) {
     return 0;
 }
 
-// the step at host_step_params' position: the column form when its history is short enough
+// an eager step that failed part-way: the attention + Wo hand-off words may hold arrivals that
+// the layer's W1/W3 launch never zeroed
+int eager_step(xh_ctx* ctx, bool with_logits, bool greedy) {
+    const int rc = enqueue_step(ctx, ctx->stream, with_logits, greedy);
+    if (rc) hipMemsetAsync(ctx->aw_sync, 0, (size_t)ctx->c.n_layers * AW_SYNC_WORDS * 4, ctx->stream);
+    return rc;
+}
+
+// the step at host_step_params' position
 int run_step(xh_ctx* ctx, bool with_logits) {
     if (with_logits) ctx->cand_valid = true;  // the lm_head launch writes candidates
-    const bool col = use_col(ctx, ctx->sp_host->kv_len);
-    if (!ctx->use_graphs) return enqueue_step(ctx, ctx->stream, with_logits, false, col);
-    hipGraphExec_t* ge = with_logits ? &ctx->g_logits[col] : &ctx->g_hydrate[col];
+    if (!ctx->use_graphs) return eager_step(ctx, with_logits, false);
+    hipGraphExec_t* ge = with_logits ? &ctx->g_logits : &ctx->g_hydrate;
     if (!*ge) {
-        int rc = capture(ctx, with_logits ? 0 : 1, col, ge);
+        int rc = capture(ctx, with_logits ? 0 : 1, ge);
         if (rc) return rc;
     }
     HIP_TRY(ctx, hipGraphLaunch(*ge, ctx->stream));
@@ -1188,12 +820,15 @@ int prefill_batched(xh_ctx* ctx, const int* tokens, int n, int pos0, int want_lo
             const size_t glu_lds = (size_t)c.hidden_dim * sizeof(float);
             bool glu_fused = false;
             if (E2 && ctx->pf_glu_split && glu_lds + 16 * sizeof(float) <= 64 * 1024) {
-                // GLU epilogue straight into the W2 GEMM's split-f16 fragments (one launch)
+                // GLU epilogue straight into the W2 GEMM's split-f16 fragments (one launch); the
+                // size check above is the launch's only precondition, so any error here is real
+                HIP_TRY(ctx, hipGetLastError());  // an earlier launch's error is reported as such
                 hipLaunchKernelGGL(prefill_glu_split_kernel, dim3(32 * ((m + 31) / 32)), dim3(1024),
                                    glu_lds, ctx->stream, (const float*)ctx->pf_part, ks,
                                    m, c.hidden_dim, c.act, E2, ctx->pf_xh, ctx->pf_xl, ctx->pf_xs);
-                glu_fused = hipGetLastError() == hipSuccess;  // a refused launch takes the two-launch path
-                ctx->pf_split_ready = glu_fused;
+                HIP_TRY(ctx, hipGetLastError());
+                glu_fused = true;
+                ctx->pf_split_ready = true;
             }
             if (!glu_fused) {
                 e = PfEpiArgs{};
@@ -1322,16 +957,8 @@ int xh_create(const xh_config* cfg, int device_ordinal, xh_ctx** out) {
     CREATE_TRY(dmalloc(ctx, &ctx->part_ml, (size_t)ctx->nsplit * c.n_heads * 2));
     CREATE_TRY(dmalloc(ctx, &ctx->attn_cnt, (size_t)c.n_kv_heads));
     CREATE_TRY(dmalloc(ctx, &ctx->aw_sync, (size_t)c.n_layers * AW_SYNC_WORDS));
-    CREATE_TRY(dmalloc(ctx, &ctx->qaw_sync, qaw_words(c)));
     CREATE_TRY(dmalloc(ctx, &ctx->cand, (size_t)ARGMAX_CANDS));
     CREATE_TRY(dmalloc(ctx, &ctx->scan_flag, (size_t)1));
-    CREATE_TRY(dmalloc(ctx, &ctx->ac_err, (size_t)1));
-    if (c.n_kv_heads <= AC_PMAX) CREATE_TRY(dmalloc(ctx, &ctx->wo_part, (size_t)c.n_kv_heads * c.dim));
-    ctx->col_kv_max = XH_COL_KV_MAX_DEFAULT;
-    // fused launch: at most 16 splits per KV head (the attention workgroups stay a small part
-    // of the 2-per-CU grid); partial buffers are sized for ctx->nsplit >= this
-    ctx->qaw_nsplit = std::min(ctx->nsplit, 16);
-    ctx->qaw_t_max = attn_split_len(c.max_seq_len, ctx->qaw_nsplit, attn_min_t(c.head_dim, QAW_THREADS));
     {
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, device_ordinal) != hipSuccess) {
@@ -1341,40 +968,8 @@ int xh_create(const xh_config* cfg, int device_ordinal, xh_ctx** out) {
         }
         ctx->n_cu = prop.multiProcessorCount;
     }
-    ctx->pk_prompt_cap = 1 << 16;
-    CREATE_TRY(dmalloc(ctx, &ctx->pk_layers, (size_t)c.n_layers));
-    CREATE_TRY(dmalloc(ctx, &ctx->pk_counters, ((size_t)c.n_layers * PK_PHASES + 1) * PK_CSLOT));
-    CREATE_TRY(dmalloc(ctx, &ctx->pk_tickets, (size_t)c.n_kv_heads));
-    CREATE_TRY(dmalloc(ctx, &ctx->pk_err, 8));
-    CREATE_TRY(dmalloc(ctx, &ctx->pk_cand, (size_t)ctx->n_cu));
-    CREATE_TRY(dmalloc(ctx, &ctx->pk_trace, std::max<size_t>(std::max<size_t>((size_t)PK_TRACE_WG * pk_trace_len(c.n_layers),
-                                                             8 * ((size_t)c.n_kv_heads * ctx->nsplit + 4096)),
-                                                             (size_t)se_trace_len(ctx->n_cu, c.n_layers))));
-    CREATE_TRY(dmalloc(ctx, &ctx->pk_prompt, (size_t)ctx->pk_prompt_cap));
-    // stream engine: ring slots that fit 160 KiB of LDS beside the control block and the
-    // attention merge area; splits per KV head: one attention item per CU at most
-    ctx->se_nslots = 0;
-    for (int ns = SE_MAXS; ns > SE_DEPTH; ns--)
-        if (se_smem_bytes(ns, ctx->qpk, c.head_dim) <= 160 * 1024) { ctx->se_nslots = ns; break; }
-    ctx->se_max_splits = std::max(1, std::min(64, ctx->n_cu / std::max(1, c.n_kv_heads)));
-    ctx->se_g_words = (size_t)c.dim + c.hidden_dim + (size_t)ctx->q_dim + ctx->n_cu;
-    CREATE_TRY(dmalloc(ctx, &ctx->se_layers, (size_t)c.n_layers));
-    CREATE_TRY(dmalloc(ctx, &ctx->se_g, ctx->se_g_words));
-    CREATE_TRY(dmalloc(ctx, &ctx->se_qcnt, (size_t)c.n_layers * c.n_kv_heads));
-    CREATE_TRY(dmalloc(ctx, &ctx->se_tickets, (size_t)c.n_kv_heads));
-    CREATE_TRY(dmalloc(ctx, &ctx->se_part_o, (size_t)ctx->se_max_splits * c.n_heads * c.head_dim));
-    CREATE_TRY(dmalloc(ctx, &ctx->se_part_ml, (size_t)ctx->se_max_splits * c.n_heads * 2));
-    if (hipHostMalloc((void**)&ctx->pk_host, (2 + (size_t)ctx->pk_prompt_cap) * sizeof(int), hipHostMallocDefault) !=
-        hipSuccess) {
-        g_create_error = "hipHostMalloc failed";
-        xh_destroy(ctx);
-        return XH_E_HIP;
-    }
-    if (hipEventCreate(&ctx->pk_ev[0]) != hipSuccess || hipEventCreate(&ctx->pk_ev[1]) != hipSuccess) {
-        g_create_error = "hipEventCreate failed";
-        xh_destroy(ctx);
-        return XH_E_HIP;
-    }
+    ctx->aw_trace_len = (size_t)8 * ((size_t)c.n_kv_heads * ctx->nsplit + 4096);
+    CREATE_TRY(dmalloc(ctx, &ctx->aw_trace, ctx->aw_trace_len));
     CREATE_TRY(dmalloc(ctx, &ctx->rope_freq, (size_t)c.head_dim / 2));
     CREATE_TRY(dmalloc(ctx, &ctx->sink_cos, (size_t)c.head_dim / 2));
     CREATE_TRY(dmalloc(ctx, &ctx->sink_sin, (size_t)c.head_dim / 2));
@@ -1421,19 +1016,12 @@ void xh_destroy(xh_ctx* ctx) {
     if (ctx->wcls && ctx->wcls != ctx->embed) hipFree(ctx->wcls);
     hipFree(ctx->embed); hipFree(ctx->final_norm);
     hipFree(ctx->kv); hipFree(ctx->x); hipFree(ctx->q); hipFree(ctx->attn_out); hipFree(ctx->hb);
-    hipFree(ctx->logits); hipFree(ctx->part_o); hipFree(ctx->part_ml); hipFree(ctx->attn_cnt); hipFree(ctx->aw_sync); hipFree(ctx->qaw_sync); hipFree(ctx->cand); hipFree(ctx->scan_flag);
-    hipFree(ctx->ac_err); hipFree(ctx->wo_part);
+    hipFree(ctx->logits); hipFree(ctx->part_o); hipFree(ctx->part_ml); hipFree(ctx->attn_cnt); hipFree(ctx->aw_sync); hipFree(ctx->cand); hipFree(ctx->scan_flag);
     hipFree(ctx->pf_tok); hipFree(ctx->pf_x); hipFree(ctx->pf_xn); hipFree(ctx->pf_q); hipFree(ctx->pf_att); hipFree(ctx->pf_h);
     hipFree(ctx->pf_xh); hipFree(ctx->pf_xl); hipFree(ctx->pf_xs);
     hipFree(ctx->pf_logits); hipFree(ctx->pf_tgt); hipFree(ctx->ppl_tgt); hipFree(ctx->ppl_prob);
     hipFree(ctx->pf_part); hipFree(ctx->pf_sp); hipFree(ctx->pf_po); hipFree(ctx->pf_pml); hipFree(ctx->pf_cnt); hipFree(ctx->rope_freq);
-    hipFree(ctx->pk_layers); hipFree(ctx->pk_counters); hipFree(ctx->pk_tickets); hipFree(ctx->pk_err);
-    hipFree(ctx->pk_cand); hipFree(ctx->pk_prompt); hipFree(ctx->pk_trace);
-    hipFree(ctx->se_layers); hipFree(ctx->se_g); hipFree(ctx->se_qcnt); hipFree(ctx->se_tickets);
-    hipFree(ctx->se_part_o); hipFree(ctx->se_part_ml);
-    if (ctx->pk_host) hipHostFree(ctx->pk_host);
-    for (hipEvent_t e : ctx->pk_ev)
-        if (e) hipEventDestroy(e);
+    hipFree(ctx->aw_trace);
     hipFree(ctx->sink_cos); hipFree(ctx->sink_sin); hipFree(ctx->sp); hipFree(ctx->dec_tokens);
     if (ctx->sp_host) hipHostFree(ctx->sp_host);
     if (ctx->stream) hipStreamDestroy(ctx->stream);
@@ -1755,12 +1343,8 @@ int xh_forward(xh_ctx* ctx, int token, int pos, int mode, float* logits_out) {
     HIP_TRY(ctx, hipSetDevice(ctx->dev));
     int rc = check_ready(ctx);
     if (rc) return rc;
-    if (use_persistent(ctx)) {
-        rc = run_persistent(ctx, &token, 1, 0, pos, mode == XH_OUTPUT_LOGITS, -1, -1, nullptr);
-    } else {
-        rc = host_step_params(ctx, token, pos);
-        if (!rc) rc = run_step(ctx, mode == XH_OUTPUT_LOGITS);
-    }
+    rc = host_step_params(ctx, token, pos);
+    if (!rc) rc = run_step(ctx, mode == XH_OUTPUT_LOGITS);
     if (rc) return rc;
     if (logits_out && mode == XH_OUTPUT_LOGITS)
         HIP_TRY(ctx, hipMemcpyAsync(logits_out, ctx->logits, (size_t)ctx->c.vocab_size * 4, hipMemcpyDeviceToHost,
@@ -1776,42 +1360,18 @@ int xh_decode_greedy(xh_ctx* ctx, int pos, int n_steps, int stop_a, int stop_b, 
     HIP_TRY(ctx, hipSetDevice(ctx->dev));
     int rc = check_ready(ctx);
     if (rc) return rc;
-    if (use_persistent(ctx)) {
-        int done = 0;
-        if (n_steps) rc = run_persistent(ctx, nullptr, 0, n_steps, pos, 1, stop_a, stop_b, &done);
-        if (rc) return rc;
-        // leave the step parameters of the last position for xh_time_kernel
-        if (done) rc = host_step_params(ctx, 0, pos + done - 1);
-        if (rc) return rc;
-        if (tokens_out && done)
-            HIP_TRY(ctx, copy_sync(ctx, tokens_out, ctx->dec_tokens, (size_t)done * sizeof(int), hipMemcpyDeviceToHost));
-        if (n_done) *n_done = done;
-        return 0;
-    }
     // step counter 0, next position `pos`; token/pos fields are set by argmax_advance_kernel
     StepParams* h = ctx->sp_host;
     h->step = 0;
     h->pos_next = pos;
     h->max_seq_len = ctx->c.max_seq_len;
     HIP_TRY(ctx, hipMemcpyAsync(&ctx->sp->step, &h->step, 3 * sizeof(int), hipMemcpyHostToDevice, ctx->stream));
-    // the step at position p has history min(p + 1, max_seq_len): the column-form graph while
-    // that is within col_kv_max
-    const int msl = ctx->c.max_seq_len;
-    auto col_at = [&](const int i) {
-        const int p = pos + i;
-        return use_col(ctx, p >= msl ? msl : p + 1);
-    };
-    if (ctx->use_graphs) {
-        for (int k = 0; k < 2; k++) {
-            const bool need = n_steps > 0 && (k ? col_at(0) : !col_at(n_steps - 1));
-            if (need && !ctx->g_decode[k]) {
-                rc = capture(ctx, 2, k == 1, &ctx->g_decode[k]);
-                if (rc) return rc;
-            }
-        }
+    if (ctx->use_graphs && n_steps > 0 && !ctx->g_decode) {
+        rc = capture(ctx, 2, &ctx->g_decode);
+        if (rc) return rc;
     }
     // the first token is the argmax of the logits on the device: candidates from them if the
-    // launch that produced them left none (persistent engine, or nothing yet)
+    // launch that produced them left none (nothing yet)
     if (!ctx->cand_valid)
         hipLaunchKernelGGL(logits_cand_kernel, dim3(1), dim3(ARGMAX_CANDS), 0, ctx->stream, (const float*)ctx->logits,
                            ctx->c.vocab_size, ctx->cand);
@@ -1819,11 +1379,10 @@ int xh_decode_greedy(xh_ctx* ctx, int pos, int n_steps, int stop_a, int stop_b, 
     const bool stops = stop_a >= 0 || stop_b >= 0;
     int done = 0;
     for (int i = 0; i < n_steps; i++) {
-        const bool col = col_at(i);
         if (ctx->use_graphs) {
-            HIP_TRY(ctx, hipGraphLaunch(ctx->g_decode[col], ctx->stream));
+            HIP_TRY(ctx, hipGraphLaunch(ctx->g_decode, ctx->stream));
         } else {
-            rc = enqueue_step(ctx, ctx->stream, true, true, col);
+            rc = eager_step(ctx, true, true);
             if (rc) return rc;
         }
         done = i + 1;
@@ -1858,7 +1417,9 @@ int xh_reset(xh_ctx* ctx) {
     HIP_TRY(ctx, hipMemsetAsync(ctx->kv, 0, (size_t)c.n_layers * 2 * c.max_seq_len * ctx->kv_dim * 2, ctx->stream));
     HIP_TRY(ctx, hipMemsetAsync(ctx->x, 0, (size_t)c.dim * 4, ctx->stream));
     HIP_TRY(ctx, hipMemsetAsync(ctx->logits, 0, (size_t)c.vocab_size * 4, ctx->stream));
-    HIP_TRY(ctx, hipMemsetAsync(ctx->qaw_sync, 0, qaw_words(c) * 4, ctx->stream));
+    // the attention + Wo hand-off words (normally zeroed by each layer's W1/W3 launch): a step
+    // that failed between the two launches must not leave a stale arrival count
+    HIP_TRY(ctx, hipMemsetAsync(ctx->aw_sync, 0, (size_t)c.n_layers * AW_SYNC_WORDS * 4, ctx->stream));
     HIP_TRY(ctx, hipMemsetAsync(ctx->cand, 0, ARGMAX_CANDS * 8, ctx->stream));
     ctx->cand_valid = true;  // all-zero candidates = zero logits (argmax token 0)
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
@@ -1914,13 +1475,7 @@ int xh_prefill(xh_ctx* ctx, const int* tokens, int n, int pos0, int want_logits,
     HIP_TRY(ctx, hipSetDevice(ctx->dev));
     int rc = check_ready(ctx);
     if (rc) return rc;
-    // the stream engine keeps the batched MFMA prompt path where it applies (16x its token loop)
-    if (use_persistent(ctx) && !(ctx->engine == 2 && pf_supported(ctx, n, pos0))) {
-        for (int off = 0; off < n && !rc; off += ctx->pk_prompt_cap) {
-            const int m = std::min(n - off, ctx->pk_prompt_cap);
-            rc = run_persistent(ctx, tokens + off, m, 0, pos0 + off, off + m == n ? want_logits : 0, -1, -1, nullptr);
-        }
-    } else if (pf_supported(ctx, n, pos0)) {
+    if (pf_supported(ctx, n, pos0)) {
         rc = prefill_batched(ctx, tokens, n, pos0, want_logits);
     } else {
         for (int i = 0; i < n && !rc; i++) {
@@ -1957,17 +1512,13 @@ int xh_perplexity(xh_ctx* ctx, const int* tokens, int n, int pos0, float* probs_
         if ((rc = dmalloc(ctx, &ctx->ppl_tgt, (size_t)m)) || (rc = dmalloc(ctx, &ctx->ppl_prob, (size_t)m))) return rc;
         ctx->ppl_cap = m;
     }
-    if ((!use_persistent(ctx) || ctx->engine == 2) && pf_supported(ctx, m, pos0)) {
+    if (pf_supported(ctx, m, pos0)) {
         rc = prefill_batched(ctx, tokens, m, pos0, 0, tokens + 1, ctx->ppl_prob);
     } else {
         HIP_TRY(ctx, copy_sync(ctx, ctx->ppl_tgt, tokens + 1, (size_t)m * sizeof(int), hipMemcpyHostToDevice));
         for (int i = 0; i < m && !rc; i++) {
-            if (use_persistent(ctx)) {
-                rc = run_persistent(ctx, tokens + i, 1, 0, pos0 + i, 1, -1, -1, nullptr);
-            } else {
-                rc = host_step_params(ctx, tokens[i], pos0 + i);
-                if (!rc) rc = run_step(ctx, true);
-            }
+            rc = host_step_params(ctx, tokens[i], pos0 + i);
+            if (!rc) rc = run_step(ctx, true);
             if (rc) break;
             hipLaunchKernelGGL(token_prob_kernel, dim3(1), dim3(1024), 0, ctx->stream, (const float*)ctx->logits, V,
                                (size_t)V, (const int*)ctx->ppl_tgt + i, ctx->ppl_prob + i);
@@ -1981,39 +1532,18 @@ int xh_perplexity(xh_ctx* ctx, const int* tokens, int n, int pos0, float* probs_
     return check_aw(ctx);
 }
 
-int xh_set_engine(xh_ctx* ctx, int engine) {
-    if (!ctx || engine < -1 || engine > 2) return XH_E_INVALID;
-    int dt, dtc, ndt;
-    if (engine == 1 && !pk_dtypes(ctx, &dt, &dtc, &ndt))
-        return set_err(ctx, XH_E_INVALID, "persistent engine not available for these weights");
-    if (engine == 2 && !se_supported(ctx, &dt, &dtc, &ndt))
-        return set_err(ctx, XH_E_INVALID, "stream engine not available for these weights");
-    ctx->engine = engine;
-    return 0;
-}
-
-int xh_last_launch_us(const xh_ctx* ctx, float* us) {
-    if (!ctx || !us) return XH_E_INVALID;
-    *us = ctx->pk_last_us;
-    return 0;
-}
-
 int xh_debug_trace(xh_ctx* ctx, int enable, uint64_t* out, int cap, int* len) {
     if (!ctx) return XH_E_INVALID;
-    const int n = std::max(std::max(PK_TRACE_WG * pk_trace_len(ctx->c.n_layers), 8 * (ctx->c.n_kv_heads * ctx->nsplit + 4096)),
-                           se_trace_len(ctx->n_cu, ctx->c.n_layers));
+    const int n = (int)ctx->aw_trace_len;
     if (len) *len = n;
     if (out && cap > 0) {
         HIP_TRY(ctx, hipSetDevice(ctx->dev));
-        HIP_TRY(ctx, copy_sync(ctx, out, ctx->pk_trace, (size_t)std::min(cap, n) * sizeof(uint64_t), hipMemcpyDeviceToHost));
+        HIP_TRY(ctx, copy_sync(ctx, out, ctx->aw_trace, (size_t)std::min(cap, n) * sizeof(uint64_t), hipMemcpyDeviceToHost));
     }
     if (enable >= 0) {
-        ctx->pk_trace_on = (enable & 1) != 0;
         ctx->aw_trace_on = (enable & 2) != 0;
-        ctx->qaw_trace_on = (enable & 4) != 0;
-        ctx->se_trace_on = (enable & 8) != 0;
         drop_graphs(ctx);
-        HIP_TRY(ctx, fill_sync(ctx, ctx->pk_trace, 0, (size_t)n * sizeof(uint64_t)));
+        HIP_TRY(ctx, fill_sync(ctx, ctx->aw_trace, 0, (size_t)n * sizeof(uint64_t)));
     }
     return 0;
 }
@@ -2021,40 +1551,25 @@ int xh_debug_trace(xh_ctx* ctx, int enable, uint64_t* out, int cap, int* len) {
 int xh_get_option(const xh_ctx* ctx, int option, int* value) {
     if (!ctx || !value) return XH_E_INVALID;
     switch (option) {
-        case XH_OPT_FUSE_ATTN_WO:
-            // effective level: 2 only while the one-launch form is instantiated for this model
-            *value = ctx->fuse_level >= 2 && ctx->qaw_ok && aw_instantiated(ctx->c.head_dim, ctx->qpk) ? 2
-                     : ctx->fuse_attn_wo ? 1 : 0;
-            return 0;
+        case XH_OPT_FUSE_ATTN_WO: *value = ctx->fuse_attn_wo ? 1 : 0; return 0;
         case XH_OPT_PREFILL: *value = ctx->prefill_batched ? ctx->prefill_gemm : 0; return 0;
         case XH_OPT_PREFILL_GLU_SPLIT: *value = ctx->pf_glu_split ? 1 : 0; return 0;
-        case XH_OPT_COL_KV_MAX: *value = col_supported(ctx) ? std::min(ctx->col_kv_max, AC_KV_MAX) : 0; return 0;
         default: return XH_E_INVALID;
     }
-}
-
-int xh_get_engine(const xh_ctx* ctx) {
-    if (!ctx) return -1;
-    return use_persistent(const_cast<xh_ctx*>(ctx)) ? ctx->engine : 0;
 }
 
 int xh_set_option(xh_ctx* ctx, int option, int value) {
     if (!ctx) return XH_E_INVALID;
     switch (option) {
         case XH_OPT_FUSE_ATTN_WO:
-            if (value < 0 || value > 2) return set_err(ctx, XH_E_INVALID, "fuse level %d not in 0..2", value);
+            if (value < 0 || value > 1) return set_err(ctx, XH_E_INVALID, "fuse level %d not in 0..1", value);
             ctx->fuse_attn_wo = value != 0;
-            ctx->fuse_level = value;
             drop_graphs(ctx);
             return 0;
         case XH_OPT_PREFILL:
             if (value < 0 || value > 3) return set_err(ctx, XH_E_INVALID, "XH_OPT_PREFILL: 0 ... 3");
             ctx->prefill_batched = value != 0;
             if (value) ctx->prefill_gemm = value;
-            return 0;
-        case XH_OPT_COL_KV_MAX:
-            if (value < 0 || value > AC_KV_MAX) return set_err(ctx, XH_E_INVALID, "XH_OPT_COL_KV_MAX: 0 ... %d", AC_KV_MAX);
-            ctx->col_kv_max = value;
             return 0;
         case XH_OPT_PREFILL_GLU_SPLIT:
             if (value < 0 || value > 1) return set_err(ctx, XH_E_INVALID, "XH_OPT_PREFILL_GLU_SPLIT: 0 or 1");
@@ -2180,8 +1695,7 @@ int xh_op_mha(float* xout, const uint16_t* kb, const uint16_t* vb, const float* 
 // timing hooks for bench.py
 // ---------------------------------------------------------------------------------------
 int xh_time_kernel(xh_ctx* ctx, int which, int iters, float* avg_us) {
-    if (!ctx || !avg_us || iters <= 0 || which < 0 || which > 7) return XH_E_INVALID;
-    if (which >= 6 && !col_supported(ctx)) return set_err(ctx, XH_E_INVALID, "column form not available");
+    if (!ctx || !avg_us || iters <= 0 || which < 0 || which > 5) return XH_E_INVALID;
     HIP_TRY(ctx, hipSetDevice(ctx->dev));
     int rc = check_ready(ctx);
     if (rc) return rc;
@@ -2198,8 +1712,6 @@ int xh_time_kernel(xh_ctx* ctx, int which, int iters, float* avg_us) {
             case 2: return launch_gemv<PRO_PLAIN, EPI_RESID>(kdt(ctx->L[l].wo_dt, ctx->L[l].wo_x), wo_args(ctx, l), ctx->stream, mb);
             case 3: return launch_gemv<PRO_PLAIN, EPI_RESID>(kdt(ctx->L[l].w2_dt, ctx->L[l].w2_x), w2_args(ctx, l), ctx->stream, mb);
             case 4: return launch_gemv<PRO_RMSNORM, EPI_LOGITS>(kdt(ctx->wcls_dt, ctx->wcls_x), cls_args(ctx), ctx->stream, mb);
-            case 6: return launch_attn_col(ctx, l, ctx->stream) == 0;
-            case 7: return launch_gemv<PRO_RMSNORM_P, EPI_GLU>(kdt(ctx->L[l].w13_dt, ctx->L[l].w13_x), w13_col_args(ctx, l), ctx->stream, mb);
             default:
                 return launch_attn(attn_args(ctx, l), ctx->c.head_dim, ctx->qpk, ctx->c.n_kv_heads, ctx->t_max,
                                    ctx->stream);
@@ -2236,10 +1748,6 @@ size_t xh_kernel_bytes(const xh_ctx* ctx, int which, int kv_len) {
         case 3: return (size_t)c.dim * file_row_bytes(w.w2_dt, c.hidden_dim) + c.hidden_dim * vec + 2 * c.dim * vec;
         case 4: return (size_t)c.vocab_size * file_row_bytes(ctx->wcls ? ctx->wcls_dt : ctx->embed_dt, c.dim) +
                        c.dim * (vec + dtype_size(ctx->final_norm_dt)) + (size_t)c.vocab_size * vec;
-        case 6: return (size_t)c.dim * file_row_bytes(w.wo_dt, ctx->q_dim) + (size_t)2 * kv_len * ctx->kv_dim * 2 +
-                       (size_t)ctx->q_dim * vec + c.dim * vec + (size_t)c.n_kv_heads * c.dim * vec;
-        case 7: return (size_t)2 * c.hidden_dim * file_row_bytes(w.w13_dt, c.dim) + c.dim * dtype_size(w.fn_dt) +
-                       (size_t)c.n_kv_heads * c.dim * vec + c.dim * vec + (size_t)c.hidden_dim * vec;
         default: return (size_t)2 * kv_len * ctx->kv_dim * 2 + 2 * (size_t)ctx->q_dim * vec;
     }
 }

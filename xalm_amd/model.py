@@ -60,7 +60,7 @@ class Model:
         if dt in L.GQ_BLOCK_BYTES and len(expected_shape) == 2 and expected_shape[1] % 32 == 0:
             # gguf blocks (convert.py:176-187): the header holds the byte shape
             expected_shape = (expected_shape[0], expected_shape[1] // 32 * L.GQ_BLOCK_BYTES[dt])
-        if tuple(ti.shape) != tuple(expected_shape):  # src/model.cpp:381-392
+        if tuple(ti.shape) != tuple(expected_shape):  # src/model.cpp:65-76
             raise ValueError(f"shape mismatch for {name}: {ti.shape} vs {expected_shape} expected!")
         if direct:
             self.upload_file(kind, layer, xf.dtype(name), xf.path, ti.offset, ti.size)
@@ -109,25 +109,9 @@ class Model:
         L.check(L.lib().xh_perplexity(self._ctx, L.ptr(toks), int(toks.size), int(pos0), L.ptr(out)), self._ctx)
         return out[: toks.size - 1]
 
-    # engine: 0 = hipGraph of kernels per token, 1 = persistent kernel, 2 = stream kernel, -1 = automatic
-    ENGINE_GRAPH, ENGINE_PERSISTENT, ENGINE_AUTO = 0, 1, -1
-
-    def set_engine(self, engine: int):
-        L.check(L.lib().xh_set_engine(self._ctx, int(engine)), self._ctx)
-
-    @property
-    def engine(self) -> int:
-        return int(L.lib().xh_get_engine(self._ctx))
-
-    def last_launch_us(self) -> float:
-        """Device time of the last persistent-engine launch (HIP events, its own stream)."""
-        v = ctypes.c_float(0.0)
-        L.check(L.lib().xh_last_launch_us(self._ctx, ctypes.byref(v)), self._ctx)
-        return float(v.value)
-
     def debug_trace(self, enable: int = -1) -> np.ndarray:
-        """Persistent-engine timeline of the last traced launch, [3][n_layers + 1][5][2] clock
-        stamps (100 MHz); `enable` 1/0 switches tracing for later launches."""
+        """Timeline of the last traced attention + Wo launch, [workgroup][8] device-clock stamps
+        (100 MHz, attn_wo.h); `enable` 2/0 switches tracing for later launches."""
         n = ctypes.c_int(0)
         L.check(L.lib().xh_debug_trace(self._ctx, -1, None, 0, ctypes.byref(n)), self._ctx)
         out = np.zeros(n.value, dtype=np.uint64)

@@ -102,7 +102,7 @@ class XalmFile:
         return bytes(self.raw("tokenizer.tokens")).split(b"\0")[:-1]
 
     def layer_tensors(self, layer: int) -> dict[int, str]:
-        """Tensor names per kind, as Model::from_xalm loads them (src/model.cpp:405-420)."""
+        """Tensor names per kind, as Model::from_xalm loads them (src/model.cpp:83-114)."""
         p = f"l.{layer}."
         return {L.ATTN_NORM: p + "attn.norm.weight", L.FFN_NORM: p + "mlp.norm.weight",
                 L.WQ: p + "attn.q.weight", L.WK: p + "attn.k.weight", L.WV: p + "attn.v.weight",
