@@ -13,12 +13,15 @@ from xalm_amd.model import InferenceState, Model  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--workload", default="mistral-7b-f16")
+    ap.add_argument("--fuse", type=int, default=1, help="XH_OPT_FUSE_ATTN_WO (2: W1/W3 role traced too)")
     args = ap.parse_args()
     w = bench.WORKLOADS[args.workload]
     c = bench.make_config(w)
     m = Model(c)
     for kind, layer, dt, seed, mean, std in bench.tensor_specs(w):
         m.upload_synthetic(kind, layer, dt, seed, mean, std)
+    from xalm_amd import _lib as L
+    m.set_option(L.OPT_FUSE_ATTN_WO, args.fuse)
     st = InferenceState(c)
     prompt = bench.prompt_tokens(c.vocab_size)
     if w["kv_prefill"]:
@@ -45,9 +48,12 @@ def main():
     nsplit = None
     # attention workgroups: stamp 1 = done (0 if it exited as an inactive split: then = start)
     nsplit = max(1, min(256 // nkv, 128, (c.max_seq_len + 255) // 256))  # attn_nsplit (xalm_hip.hip)
+    # Wo workgroups (AwShape: 16 waves x 2 rows, one round of <= 4096 waves): ceil(dim / 32)
+    nb_wo = (c.dim + 31) // 32
     att = [i for i in used if i < nkv * nsplit]
-    wo = [i for i in used if i >= nkv * nsplit]
-    print(f"workgroups traced: {len(used)} (attention {len(att)}, wo {len(wo)})")
+    wo = [i for i in used if nkv * nsplit <= i < nkv * nsplit + nb_wo]
+    mlp = [i for i in used if i >= nkv * nsplit + nb_wo]
+    print(f"workgroups traced: {len(used)} (attention {len(att)}, wo {len(wo)}, w1/w3 {len(mlp)})")
     if att:
         a_start = np.array([us(t[i, 0]) for i in att])
         a_done = np.array([us(t[i, 1]) for i in att if t[i, 1]])
@@ -68,9 +74,19 @@ def main():
             if v.size:
                 print(f"  {name:15s} min {v.min():6.2f} med {np.median(v):6.2f} max {v.max():6.2f} us")
     if wo:
-        for k, name in ((0, "wo start"), (1, "wo passed"), (3, "wo staged"), (2, "wo end")):
-            v = np.array([us(t[i, k]) for i in wo])
-            print(f"{name:15s}  min {v.min():6.2f} med {np.median(v):6.2f} max {v.max():6.2f} us")
+        for k, name in ((0, "wo start"), (1, "wo passed"), (3, "wo staged"), (2, "wo end"), (4, "wo x published")):
+            v = np.array([us(t[i, k]) for i in wo if t[i, k]])
+            if v.size:
+                print(f"{name:15s}  min {v.min():6.2f} med {np.median(v):6.2f} max {v.max():6.2f} us")
+    if mlp:
+        for k, name in ((0, "w13 start"), (1, "w13 x ready"), (2, "w13 end")):
+            v = np.array([us(t[i, k]) for i in mlp if t[i, k]])
+            if v.size:
+                q = np.percentile(v, [10, 50, 90])
+                print(f"{name:15s}  min {v.min():6.2f} p10 {q[0]:6.2f} med {q[1]:6.2f} p90 {q[2]:6.2f} max {v.max():6.2f} us")
+        st_ = np.array(sorted(us(t[i, 0]) for i in mlp))
+        print("w13 workgroups started by 2/5/10/15/20/30 us:",
+              [int((st_ <= x).sum()) for x in (2, 5, 10, 15, 20, 30)], "of", len(mlp))
     m.close()
 
 
