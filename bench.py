@@ -283,6 +283,8 @@ def main():
                     help="also time xh_prefill of this many prompt tokens (batched f32-MFMA path; 0 = skip)")
     ap.add_argument("--fuse-attn-wo", type=int, default=1, choices=(0, 1, 2),
                     help="attention + Wo + W1/W3 in one launch (2), attention + Wo (1), separate launches (0)")
+    ap.add_argument("--balance", type=int, default=-1, choices=(-1, 0, 1),
+                    help="XH_OPT_BALANCE: one workgroup per CU for qkv and W1/W3 (-1 = library default)")
     ap.add_argument("--fuse-mlp", type=int, default=-1, choices=(-1, 0, 1),
                     help="W1/W3 + W2 in one launch (1) or two (0); -1 = library default")
     args = ap.parse_args()
@@ -307,6 +309,8 @@ def main():
         model.upload_synthetic(kind, layer, dt, seed, mean, std)
 
     model.set_option(L.OPT_FUSE_ATTN_WO, args.fuse_attn_wo)
+    if args.balance >= 0:
+        model.set_option(L.OPT_BALANCE, args.balance)
     if args.fuse_mlp >= 0:
         model.set_option(L.OPT_FUSE_MLP, args.fuse_mlp)
     prompt = prompt_tokens(c.vocab_size)

@@ -196,7 +196,10 @@ int xh_set_graphs(xh_ctx* ctx, int enable);
  * (mlp.h): the W2 rows' weight stream starts under the W1/W3 stream with an in-launch hand-off of
  * hb, where both share a dtype and the rows divide into the pipelined steps (else two launches).
  * Same math. */
-enum xh_option { XH_OPT_FUSE_ATTN_WO = 1, XH_OPT_PREFILL = 2, XH_OPT_PREFILL_GLU_SPLIT = 3, XH_OPT_FUSE_MLP = 4 };
+/* XH_OPT_BALANCE: the qkv and W1/W3 matvecs run one workgroup per CU with the same number of
+ * row groups on every CU where the row count allows it (12 / 14 waves per workgroup). */
+enum xh_option { XH_OPT_FUSE_ATTN_WO = 1, XH_OPT_PREFILL = 2, XH_OPT_PREFILL_GLU_SPLIT = 3, XH_OPT_FUSE_MLP = 4,
+                 XH_OPT_BALANCE = 5 };
 int xh_set_option(xh_ctx* ctx, int option, int value);
 int xh_get_option(const xh_ctx* ctx, int option, int* value);
 

@@ -29,6 +29,9 @@ enum { PRO_PLAIN = 0, PRO_RMSNORM = 1 };
 enum { EPI_STORE = 0, EPI_RESID = 1, EPI_QKV = 2, EPI_GLU = 3, EPI_LOGITS = 4 };
 
 constexpr int LDS_HEAD_BYTES = 64;  // block-reduction scratch in front of the x image
+#ifndef GEMV_PRE2
+#define GEMV_PRE2 1  // PIPE-2 PF prologue requests two weight steps (gemv_body)
+#endif
 // attn_wo.h hand-off words of a layer that the launch after it zeroes (every 32nd word)
 constexpr int AW_RESET_WORDS = 18;
 constexpr int MLP_RESET_WORDS = 9;  // mlp.h: [0] arrivals, [32 (1 + k)] per-XCD flags
@@ -811,7 +814,16 @@ __device__ __forceinline__ void gemv_body(const GemvArgs& a, const int block, co
         const bool prefetched = g < n_groups;
         u32x4 pre[S::U][S::ROWS];
         float pre_d[S::U][S::ROWS];
-        gemv_prefetch<S>(a, min(g, n_groups - 1), lane, pre);
+        // PIPE 2 with plain weights: both register sets requested inside the prologue (two
+        // steps in flight while x is staged, as after it)
+        constexpr bool PRE2 = S::PIPE == 2 && WScale<DT>::BLOCK == 0 && GEMV_PRE2;
+        u32x4 pre2[S::U][S::ROWS];
+        if constexpr (PRE2) {
+            pipe_load_step<S, E>(a, min(g, n_groups - 1), n_blocks * S::WAVES, lane, pre, 0);
+            pipe_load_step<S, E>(a, min(g, n_groups - 1), n_blocks * S::WAVES, lane, pre2, 1);
+        } else {
+            gemv_prefetch<S>(a, min(g, n_groups - 1), lane, pre);
+        }
         if constexpr (WScale<DT>::BLOCK > 0) {
             size_t rs;
             const char* wrow = gemv_row_ptr<S::ROWS>(a, min(g, n_groups - 1), lane, rs);
@@ -821,7 +833,10 @@ __device__ __forceinline__ void gemv_body(const GemvArgs& a, const int block, co
         if (EPI == EPI_QKV && block == 0) rotate_sinks<S::THREADS>(a, a.sp->kv_sink);
         __syncthreads();
         if (a.trace && threadIdx.x == 0) a.trace[4 * block + 1] = __builtin_amdgcn_s_memrealtime();
-        if constexpr (S::PIPE == 2) {
+        if constexpr (PRE2) {
+            if (prefetched)
+                gemv_rows_pipe<DT, EPI, S, true, SC1, true>(a, g, n_blocks * S::WAVES, lane, xs4, pre, &best, nullptr, pre2);
+        } else if constexpr (S::PIPE == 2) {
             if (prefetched) gemv_rows_pipe<DT, EPI, S, true, SC1>(a, g, n_blocks * S::WAVES, lane, xs4, pre, &best, pre_d);
         } else {
             if (prefetched) gemv_rows<DT, EPI, S, true, SC1>(a, g, n_blocks * S::WAVES, lane, xs4, pre, &best);

@@ -153,12 +153,16 @@ struct xh_ctx {
     // (tools/gemv_bench GB_T1K: 10.95 -> 10.12 us f16, 7.93 -> 7.34 us fp8)
     int qkv_waves = 2048;
     int n_cu = 0;
+    bool balance = false;  // XH_OPT_BALANCE: one workgroup per CU for qkv / W1/W3 (ShapeB12 / B14)
     // attn_wo.h debug timeline (xh_debug_trace): [workgroup][8] device-clock stamps
     unsigned long long* aw_trace = nullptr;
     size_t aw_trace_len = 0;
     bool aw_trace_on = false;
     bool mlp_trace_on = false;  // fused W1/W3 + W2 launches write aw_trace ([workgroup][4])
     bool w13_trace_on = false;  // plain W1/W3 launches write aw_trace ([workgroup][4])
+    // the last layer's launches and the lm_head each write their own region of aw_trace
+    // (LT_QKV ...): the step's timeline, kernel boundaries included (tools/layer_trace.py)
+    bool layer_trace_on = false;
     uint16_t* kcache(int l) { return kv + (size_t)l * 2 * c.max_seq_len * kv_dim; }
     uint16_t* vcache(int l) { return kcache(l) + (size_t)c.max_seq_len * kv_dim; }
 };
@@ -234,6 +238,14 @@ void launch_gemv_s(const GemvArgs& a, hipStream_t s, int max_waves) {
 // 568 -> 584 tok/s (their 4 KiB rows are one step per group, so a wave drained to zero at
 // every group), f16 unchanged (383 / 383); W2, Wo and lm_head unchanged either way
 using ShapePF2P = GemvShape<512, ROWS, UNROLL, true, 4, true, 2, 2>;  // n <= 4096
+// One workgroup per CU with the same row-group count on every CU (the 512-thread grids of qkv
+// and W1/W3 leave CUs with one workgroup idle for the last third of the launch, or unused:
+// tools/balance_trace.py): 12 waves x 1 group (qkv of Mistral / Llama: 3072 groups on 256 CUs),
+// 14 waves x 4 groups (W1/W3: 14336 groups)
+using ShapeB12 = GemvShape<768, ROWS, UNROLL, true, 3, true, 2, 2>;
+using ShapeB14 = GemvShape<896, ROWS, UNROLL, true, 4, true, 2, 2>;
+// CUs to balance over (XH_OPT_BALANCE; 0 = the 512-thread shapes)
+thread_local int g_balance_cu = 0;
 
 
 template <int DT, int PRO, int EPI>
@@ -244,8 +256,15 @@ void launch_gemv_t(const GemvArgs& a, hipStream_t s, int max_waves) {
     // PF needs whole first chunks (n >= 64 E U) and x in XN float4 per thread
     const bool pf = !gq_dt(DT) && a.n % 4 == 0 && a.n >= 64 * E * UNROLL;
     if constexpr ((EPI == EPI_QKV || EPI == EPI_GLU) && !gq_dt(DT)) {
-        if (pf && a.n / 4 <= 2 * 512 && a.n % (64 * E * UNROLL) == 0)
+        if (pf && a.n / 4 <= 2 * 512 && a.n % (64 * E * UNROLL) == 0) {
+            const int groups = (a.rows + ROWS - 1) / ROWS, cu = g_balance_cu;
+            if (cu > 0 && groups % cu == 0) {
+                const int gpc = groups / cu;  // row groups per CU
+                if (gpc % 12 == 0 && gpc / 12 <= 8) return launch_gemv_s<DT, PRO, EPI, ShapeB12>(a, s, 12 * cu);
+                if (gpc % 14 == 0 && gpc / 14 <= 8) return launch_gemv_s<DT, PRO, EPI, ShapeB14>(a, s, 14 * cu);
+            }
             return launch_gemv_s<DT, PRO, EPI, ShapePF2P>(a, s, max_waves);
+        }
     }
     if constexpr (gq_dt(DT)) {
         // gguf blocks: the pipelined PF shapes with the block scales loaded beside the codes.
@@ -344,6 +363,10 @@ int attn_nsplit(int n_kv_heads, int max_seq_len) {
 // ---------------------------------------------------------------------------------------
 // the per-token step, enqueued on a stream (eager or under graph capture)
 // ---------------------------------------------------------------------------------------
+// debug layer timeline: regions of aw_trace (words) per launch of the traced (last) layer
+constexpr size_t LT_QKV = 0, LT_AW = 8192, LT_W13 = 16384, LT_W2 = 20480, LT_CLS = 24576, LT_WORDS = 28672;
+bool layer_traced(const xh_ctx* ctx, int l) { return ctx->layer_trace_on && l == ctx->c.n_layers - 1; }
+
 GemvArgs qkv_args(xh_ctx* ctx, int l) {
     const LayerW& w = ctx->L[l];
     GemvArgs a{};
@@ -356,6 +379,7 @@ GemvArgs qkv_args(xh_ctx* ctx, int l) {
     a.qkv_clip = ctx->c.qkv_clip; a.sp = ctx->sp;
     // the layer's MLP hand-off words start at zero for its fused W1/W3 + W2 launch
     if (ctx->fuse_mlp) a.mlp_reset = ctx->mlp_sync + (size_t)MLP_SYNC_WORDS * l;
+    if (layer_traced(ctx, l)) a.trace = ctx->aw_trace + LT_QKV;
     return a;
 }
 GemvArgs wo_args(xh_ctx* ctx, int l) {
@@ -374,6 +398,7 @@ GemvArgs w13_args(xh_ctx* ctx, int l) {
     a.out = ctx->hb; a.act = ctx->c.act; a.sp = ctx->sp;
     // debug timeline of the plain W1/W3 launch ([workgroup][4]; the fused MLP launch writes its own)
     if (ctx->w13_trace_on) a.trace = ctx->aw_trace;
+    if (layer_traced(ctx, l)) a.trace = ctx->aw_trace + LT_W13;
     return a;
 }
 GemvArgs w2_args(xh_ctx* ctx, int l) {
@@ -381,6 +406,7 @@ GemvArgs w2_args(xh_ctx* ctx, int l) {
     GemvArgs a{};
     a.w = w.w2; a.row_bytes = dev_row_bytes(w.w2_dt, ctx->c.hidden_dim);
     a.n = ctx->c.hidden_dim; a.rows = ctx->c.dim; a.x = ctx->hb; a.out = ctx->x; a.sp = ctx->sp;
+    if (layer_traced(ctx, l)) a.trace = ctx->aw_trace + LT_W2;
     return a;
 }
 GemvArgs cls_args(xh_ctx* ctx) {
@@ -389,6 +415,7 @@ GemvArgs cls_args(xh_ctx* ctx) {
     a.n = ctx->c.dim; a.rows = ctx->c.vocab_size; a.x = ctx->x;
     a.norm_w = ctx->final_norm; a.norm_dtype = ctx->final_norm_dt; a.eps = ctx->c.norm_eps;
     a.out = ctx->logits; a.sp = ctx->sp; a.cand = ctx->cand;
+    if (ctx->layer_trace_on) a.trace = ctx->aw_trace + LT_CLS;
     return a;
 }
 AttnArgs attn_args(xh_ctx* ctx, int l) {
@@ -453,7 +480,7 @@ int launch_attn_wo(xh_ctx* ctx, int l, hipStream_t s, bool mlp = false) {
     unsigned* sync = ctx->aw_sync + (size_t)AW_SYNC_WORDS * l;
     const int hd = ctx->c.head_dim, qpk = ctx->qpk, nkv = ctx->c.n_kv_heads, tm = ctx->t_max_aw;
     const int mw = ctx->max_gemv_waves;
-    unsigned long long* tr = ctx->aw_trace_on ? ctx->aw_trace : nullptr;
+    unsigned long long* tr = ctx->aw_trace_on ? ctx->aw_trace : layer_traced(ctx, l) ? ctx->aw_trace + LT_AW : nullptr;
     switch (ctx->L[l].wo_dt) {
         case XH_F32: return aw_launch_dt1(aa, ga, ma, hd, qpk, nkv, tm, sync, mw, s, tr);
         case XH_F16: return aw_launch_dt2(aa, ga, ma, hd, qpk, nkv, tm, sync, mw, s, tr);
@@ -507,6 +534,7 @@ int check_aw(xh_ctx* ctx) {
 // greedy: the token is the argmax of the previous step's logits (argmax_embed_kernel)
 int enqueue_step(xh_ctx* ctx, hipStream_t s, bool with_logits, bool greedy = false) {
     const xh_config& c = ctx->c;
+    g_balance_cu = ctx->balance ? ctx->n_cu : 0;
     const int mb = ctx->max_gemv_waves;
     if (greedy)
         hipLaunchKernelGGL(argmax_embed_kernel, dim3(1), dim3(ARGMAX_CANDS), 0, s, (const unsigned long long*)ctx->cand,
@@ -1605,6 +1633,7 @@ int xh_debug_trace(xh_ctx* ctx, int enable, uint64_t* out, int cap, int* len) {
         ctx->aw_trace_on = (enable & 2) != 0;
         ctx->mlp_trace_on = (enable & 4) != 0;
         ctx->w13_trace_on = (enable & 8) != 0;
+        ctx->layer_trace_on = (enable & 16) != 0 && ctx->aw_trace_len >= LT_WORDS;
         drop_graphs(ctx);
         HIP_TRY(ctx, fill_sync(ctx, ctx->aw_trace, 0, (size_t)n * sizeof(uint64_t)));
     }
@@ -1618,6 +1647,7 @@ int xh_get_option(const xh_ctx* ctx, int option, int* value) {
         case XH_OPT_PREFILL: *value = ctx->prefill_batched ? ctx->prefill_gemm : 0; return 0;
         case XH_OPT_PREFILL_GLU_SPLIT: *value = ctx->pf_glu_split ? 1 : 0; return 0;
         case XH_OPT_FUSE_MLP: *value = ctx->fuse_mlp ? 1 : 0; return 0;
+        case XH_OPT_BALANCE: *value = ctx->balance ? 1 : 0; return 0;
         default: return XH_E_INVALID;
     }
 }
@@ -1635,6 +1665,11 @@ int xh_set_option(xh_ctx* ctx, int option, int value) {
             if (value < 0 || value > 3) return set_err(ctx, XH_E_INVALID, "XH_OPT_PREFILL: 0 ... 3");
             ctx->prefill_batched = value != 0;
             if (value) ctx->prefill_gemm = value;
+            return 0;
+        case XH_OPT_BALANCE:
+            if (value < 0 || value > 1) return set_err(ctx, XH_E_INVALID, "XH_OPT_BALANCE: 0 or 1");
+            ctx->balance = value != 0;
+            drop_graphs(ctx);
             return 0;
         case XH_OPT_FUSE_MLP:
             if (value < 0 || value > 1) return set_err(ctx, XH_E_INVALID, "XH_OPT_FUSE_MLP: 0 or 1");
@@ -1772,6 +1807,7 @@ int xh_time_kernel(xh_ctx* ctx, int which, int iters, float* avg_us) {
     int rc = check_ready(ctx);
     if (rc) return rc;
     const int mb = ctx->max_gemv_waves;
+    g_balance_cu = ctx->balance ? ctx->n_cu : 0;
     // launches rotate over the layers, so a repeat never finds its weights in the 256 MB
     // Infinity Cache (a decode step streams every layer once)
     int rot = 0;
