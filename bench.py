@@ -281,12 +281,8 @@ def main():
                          "wherever the weights allow, 3 f32-input MFMA only")
     ap.add_argument("--prefill-tokens", type=int, default=512,
                     help="also time xh_prefill of this many prompt tokens (batched f32-MFMA path; 0 = skip)")
-    ap.add_argument("--fuse-attn-wo", type=int, default=1, choices=(0, 1, 2),
-                    help="attention + Wo + W1/W3 in one launch (2), attention + Wo (1), separate launches (0)")
-    ap.add_argument("--balance", type=int, default=-1, choices=(-1, 0, 1),
-                    help="XH_OPT_BALANCE: one workgroup per CU for qkv and W1/W3 (-1 = library default)")
-    ap.add_argument("--fuse-mlp", type=int, default=-1, choices=(-1, 0, 1),
-                    help="W1/W3 + W2 in one launch (1) or two (0); -1 = library default")
+    ap.add_argument("--fuse-attn-wo", type=int, default=1, choices=(0, 1),
+                    help="attention + Wo in one launch (1) or two launches (0)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -309,10 +305,6 @@ def main():
         model.upload_synthetic(kind, layer, dt, seed, mean, std)
 
     model.set_option(L.OPT_FUSE_ATTN_WO, args.fuse_attn_wo)
-    if args.balance >= 0:
-        model.set_option(L.OPT_BALANCE, args.balance)
-    if args.fuse_mlp >= 0:
-        model.set_option(L.OPT_FUSE_MLP, args.fuse_mlp)
     prompt = prompt_tokens(c.vocab_size)
     st = InferenceState(c)
     pos0 = 0
@@ -416,8 +408,7 @@ def main():
             "data": "synthetic (deterministic xalm_synth weights of the named shapes; no checkpoint offline)",
             "config": {"workload": w["desc"], "prompt_tokens": len(prompt), "max_seq_len": c.max_seq_len,
                        "kv_len_timed": [pos + 1, pos + args.steps], "batch": 1, "parallelism": f"replicas x{world}",
-                       "engine": {2: "hipGraph per token, attention+Wo+W1/W3 fused",
-                                  1: "hipGraph per token, attention+Wo fused",
+                       "engine": {1: "hipGraph per token, attention+Wo fused",
                                   0: "hipGraph per token"}[model.get_option(L.OPT_FUSE_ATTN_WO)]},
             "roofline": roofline,
             "hbm_step": {"achieved_GBps": round(step_gbps, 1), "frac": round(step_gbps / HBM_PEAK_GBPS, 4),

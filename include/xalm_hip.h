@@ -153,10 +153,12 @@ int xh_prefill(xh_ctx* ctx, const int* tokens, int n, int pos0, int want_logits,
  * reference does in double. */
 int xh_perplexity(xh_ctx* ctx, const int* tokens, int n, int pos0, float* probs_out);
 
-/* Debug timeline of the fused attention + Wo launches.  enable: 2 = on (every attn_wo launch
- * writes [workgroup][8] device-clock stamps, 100 MHz: start, attention done / hand-off passed,
- * end, split known, scores done, p.V done, partial drained; each launch overwrites), 0 = off,
- * -1 = unchanged.  Copies min(cap, *len) words of the last traced launch to `out` first. */
+/* Debug timelines (device clock, 100 MHz; each launch overwrites).  enable bits: 2 = every
+ * attention + Wo launch writes [workgroup][8] stamps (start, attention done / hand-off passed,
+ * end, split known, scores done, p.V done, partial drained); 8 = every W1/W3 launch writes
+ * [workgroup][4] (start, x staged, end, XCD << 32 | HW_ID); 16 = the last layer's launches and the
+ * lm_head write [workgroup][4 | 8] into their own regions (tools/layer_trace.py); 0 = off,
+ * -1 = unchanged.  Copies min(cap, *len) words of the trace buffer to `out` first. */
 int xh_debug_trace(xh_ctx* ctx, int enable, uint64_t* out, int cap, int* len);
 
 /* Copy the current device logits to the host. */
@@ -177,10 +179,7 @@ size_t xh_active_bytes(const xh_ctx* ctx, size_t pos);
 int xh_set_graphs(xh_ctx* ctx, int enable);
 
 /* Launch-structure variants.  XH_OPT_FUSE_ATTN_WO (default 1): 1 = attention and Wo (+ residual)
- * in one launch with an in-launch hand-off (attn_wo.h); 2 = the layer's W1/W3 matvec (+ rmsnorm,
- * SwiGLU/GELU) joins that launch behind a second hand-off (its weight stream starts during the
- * attention chain), where Wo and W1/W3 share a dtype and dim <= 4096 divides into its steps,
- * else level 1 for that layer; 0 = separate launches.  Same math. */
+ * in one launch with an in-launch hand-off (attn_wo.h); 0 = two launches.  Same math. */
 /* XH_OPT_PREFILL (default 1): xh_prefill / xh_perplexity process the prompt in passes of up to
  * 64 tokens, each weight matrix streamed once per pass into MFMA GEMMs (prefill.h): 1 = f32-input
  * MFMA (activations exactly as the reference), except fp8 weights, which take the split-f16
@@ -192,14 +191,7 @@ int xh_set_graphs(xh_ctx* ctx, int enable);
  * epilogue of the W1/W3 GEMM writes those f16 hi/lo fragments directly (one launch); 0 = GLU to
  * f32 first, then split in the W2 GEMM's input pass (two launches).  Bit-identical results; a
  * debug knob so tests cover both routes. */
-/* XH_OPT_FUSE_MLP (default 0): the feed-forward block's W1/W3 and W2 matvecs in one launch
- * (mlp.h): the W2 rows' weight stream starts under the W1/W3 stream with an in-launch hand-off of
- * hb, where both share a dtype and the rows divide into the pipelined steps (else two launches).
- * Same math. */
-/* XH_OPT_BALANCE: the qkv and W1/W3 matvecs run one workgroup per CU with the same number of
- * row groups on every CU where the row count allows it (12 / 14 waves per workgroup). */
-enum xh_option { XH_OPT_FUSE_ATTN_WO = 1, XH_OPT_PREFILL = 2, XH_OPT_PREFILL_GLU_SPLIT = 3, XH_OPT_FUSE_MLP = 4,
-                 XH_OPT_BALANCE = 5 };
+enum xh_option { XH_OPT_FUSE_ATTN_WO = 1, XH_OPT_PREFILL = 2, XH_OPT_PREFILL_GLU_SPLIT = 3 };
 int xh_set_option(xh_ctx* ctx, int option, int value);
 int xh_get_option(const xh_ctx* ctx, int option, int* value);
 
@@ -216,10 +208,9 @@ int xh_op_mha(float* xout, const uint16_t* kb, const uint16_t* vb, const float* 
 
 /* ---- timing hooks used by bench.py (HIP events on the context's own stream) -------- */
 /* Average device time (microseconds) of one launch of kernel `which` (0 = the fused
- * gate/up matvec, 1 = qkv, 2 = wo, 3 = down, 4 = lm_head, 5 = attention, 6 = the fuse-level-2
- * attention + Wo + W1/W3 launch followed by its layer's W2 launch, as a pair: subtract 3) over
- * `iters` back-to-back launches with the current step parameters (layers rotate, so the
- * Infinity Cache never serves a repeat). */
+ * gate/up matvec, 1 = qkv, 2 = wo, 3 = down, 4 = lm_head, 5 = attention) over `iters`
+ * back-to-back launches with the current step parameters (layers rotate, so the Infinity Cache
+ * never serves a repeat). */
 int xh_time_kernel(xh_ctx* ctx, int which, int iters, float* avg_us);
 /* Bytes one launch of that kernel must move (algorithmic). */
 size_t xh_kernel_bytes(const xh_ctx* ctx, int which, int kv_len);

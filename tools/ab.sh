@@ -1,7 +1,7 @@
 set -u
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
-# usage: WL="workloads" ARGS_A=".." ARGS_B=".." LIB_A=path LIB_B=path bash tools/ab_fuse.sh  (alternating A/B)
+# usage: WL="workloads" ARGS_A=".." ARGS_B=".." LIB_A=path LIB_B=path bash tools/ab.sh  (alternating A/B)
 WL=${WL:-mistral-7b-f16 mistral-7b-f8}
 for w in $WL; do for v in A B A B; do
   if [ $v = A ]; then a=${ARGS_A:-}; lib=${LIB_A:-}; else a=${ARGS_B:-}; lib=${LIB_B:-}; fi

@@ -8,7 +8,6 @@ import numpy as np
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import bench  # noqa: E402
-from xalm_amd import _lib as L  # noqa: E402
 from xalm_amd.model import InferenceState, Model  # noqa: E402
 
 
@@ -21,7 +20,6 @@ def main():
     m = Model(c)
     for kind, layer, dt, seed, mean, std in bench.tensor_specs(w):
         m.upload_synthetic(kind, layer, dt, seed, mean, std)
-    m.set_option(L.OPT_FUSE_MLP, 0)
     st = InferenceState(c)
     prompt = bench.prompt_tokens(c.vocab_size)
     m.prefill(prompt, 0, st)

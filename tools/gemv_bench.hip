@@ -102,7 +102,23 @@ int main(int argc, char** argv) {
     // W2-shaped (n = 14336) launch shapes: x in 8 float4 per thread; PIPE 2 needs n % (64 E U) == 0
 #define VW2(NAME, MW, R, U, P) {NAME, [](const Mat& m, const GemvArgs& a) { \
         if (m.n > 4096) launch_any<GemvShape<512, R, U, true, 4, true, 8, P>>(m, a, MW); }}
-    std::vector<Variant> vs = getenv("GB_W2") ? std::vector<Variant>{
+#define VW2T(NAME, MW, T, R, U, P) {NAME, [](const Mat& m, const GemvArgs& a) { \
+        if (m.n > 4096) launch_any<GemvShape<T, R, U, true, 4, true, (14336 / 4 + T - 1) / T, P>>(m, a, MW); }}
+    // per-CU balance (GB_BAL): the product's 512-thread grids give W1/W3 448 workgroups (64 CUs
+    // with one, 192 with two) and qkv 192; these give every CU the same row-group count
+#define VB(NAME, MW, T, MINW) {NAME, [](const Mat& m, const GemvArgs& a) { \
+        if (m.n <= 4096) launch_any<GemvShape<T, 2, 4, true, MINW, true, (4096 / 4 + T - 1) / T, 2>>(m, a, MW); }}
+    std::vector<Variant> vs = getenv("GB_BAL") ? std::vector<Variant>{
+        VPP("t512 r2 u4 pf pipe2 (product)", 4096, 512, 2, 4, 4),
+        VPP("t512 w2048 (product qkv)", 2048, 512, 2, 4, 4),
+        VB("t448 w3584 (2/CU x 7 waves)", 3584, 448, 4),
+        VB("t896 w3584 (1/CU x 14)", 3584, 896, 4),
+        VB("t384 w3072 (2/CU x 6)", 3072, 384, 3),
+        VB("t768 w3072 (1/CU x 12)", 3072, 768, 3),
+        VB("t512 w4096 (2/CU x 8)", 4096, 512, 4),
+        VB("t256 w4096 (4/CU x 4)", 4096, 256, 4),
+        VB("t448 w1792 (1/CU x 7)", 1792, 448, 2),
+    } : getenv("GB_W2") ? std::vector<Variant>{
         VW2("w2 r2 u4 (product)", 4096, 2, 4, 1),
         VW2("w2 r2 u7", 4096, 2, 7, 1),
         VW2("w2 r2 u7 pipe2", 4096, 2, 7, 2),
@@ -111,6 +127,12 @@ int main(int argc, char** argv) {
         VW2("w2 r2 u4 pipe2 (f16 only)", 4096, 2, 4, 2),
         VW2("w2 r1 u4", 4096, 1, 4, 1),
         VW2("w2 r2 u7 pipe2 w2048", 2048, 2, 7, 2),
+        VW2T("w2 t256 r2 u4 w2048 (2/CU x 4)", 2048, 256, 2, 4, 1),
+        VW2T("w2 t512 r1 u4 w4096", 4096, 512, 1, 4, 1),
+        VW2T("w2 t256 r1 u4 w4096 (4/CU x 4)", 4096, 256, 1, 4, 1),
+        VW2T("w2 t384 r1 u4 w3072 (2/CU x 6)", 3072, 384, 1, 4, 1),
+        VW2T("w2 t1024 r1 u4 w4096 (1/CU)", 4096, 1024, 1, 4, 1),
+        VW2T("w2 t256 r2 u4 pipe2 w2048 (f16 only)", 2048, 256, 2, 4, 2),
     } : getenv("GB_T1K") ? std::vector<Variant>{
         VPP("t512 r2 u4 pf pipe2 (product)", 4096, 512, 2, 4, 4),
         VPK("t1024 r2 u4 pipe2 w4096", 4096, 2, 4),
@@ -151,6 +173,7 @@ int main(int argc, char** argv) {
             for (size_t vi = 0; vi < vs.size(); vi++) {
                 const Mat& m = mats[mi];
                 if (getenv("GB_W2") && m.n <= 4096) continue;
+                if (getenv("GB_BAL") && m.n > 4096) continue;
                 if (getenv("GB_W2") && DT != XH_F16 && vs[vi].name.find("f16 only") != std::string::npos) continue;
                 if (m.n > 8192 && std::string(vs[vi].name).find("t128") == 0) continue;
                 GemvArgs a{};

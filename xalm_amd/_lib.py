@@ -31,8 +31,6 @@ def row_bytes(dtype: int, n: int) -> int:
 OPT_FUSE_ATTN_WO = 1
 OPT_PREFILL = 2
 OPT_PREFILL_GLU_SPLIT = 3
-OPT_FUSE_MLP = 4
-OPT_BALANCE = 5
 
 # enum xh_tensor_kind
 EMBED, ATTN_NORM, FFN_NORM, WQ, WK, WV, WO, W1, W2, W3, FINAL_NORM, WCLS = range(12)

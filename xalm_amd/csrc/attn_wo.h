@@ -14,19 +14,10 @@
 //   loads, s_sleep, 2 s bound), then the workgroup merges the partials while staging its x
 //   image (out = sum_s e^{m_s-M} o_s / sum_s e^{m_s-M} l_s, as attention.h's merge) with sc1
 //   loads, and finishes the rows;
-// * MLP (optional): the W1/W3 matvec of the layer joins the launch as a third role.  Its
-//   workgroups follow the Wo ones, so the first of them land on the CUs the short-history
-//   attention leaves idle and request their first two weight steps (16 KiB per wave) while the
-//   attention chain runs, instead of after a kernel boundary (the chain leaves HBM idle for
-//   ~5 us per layer at 4k).  The Wo workgroups store x write-through, drain and arrive on
-//   sync[AW_XCNT]; the last arrival sets one "x ready" flag per XCD; the W1/W3 workgroups poll
-//   it, stage rmsnorm(x) with sc1 loads (gemv_after) and stream the rest of their rows;
-// * the next launch on the stream (W1/W3 of the layer, or W2 with MLP; GemvArgs::aw_reset)
-//   zeroes sync[] for the next use.
-// Attention workgroups are dispatched first (lowest block ids) and never wait on anything; Wo
-// workgroups wait only on them, W1/W3 workgroups only on the Wo ones; dispatch is in block
-// order, so progress does not depend on co-residency.  Fan-in: n_kv_heads * n_active arrivals
-// (heads), nb_wo arrivals (x).
+// * the next launch on the stream (W1/W3 of the layer, GemvArgs::aw_reset) zeroes sync[] for
+//   the next use.
+// Attention workgroups are dispatched first (lowest block ids) and never wait on anything, so
+// progress does not depend on co-residency.  Fan-in: n_kv_heads * n_active arrivals.
 #pragma once
 
 #include "attention.h"
@@ -46,25 +37,11 @@ using AwShape = GemvShape<AW_THREADS, 2, (WDec<DT>::E >= 16 ? 4 : 8), true, 4, t
 // sync (AW_SYNC_WORDS per layer): [0] head arrivals, [2] timeout flag (sticky, host-checked),
 // [AW_FLAG0 + 32 k] "heads done" flag of XCD k: set by the last head arrival, polled by that
 // XCD's Wo workgroups (one polled line per XCD instead of every Wo workgroup polling the
-// counter the arrivals add to); MLP: [AW_XCNT] Wo arrivals, [AW_XFLAG0 + 32 k] "x ready" flag
-// of XCD k.  Every 32nd word up to AW_RESET_WORDS is zeroed by the next launch.
+// counter the arrivals add to).  Words 0, 32, ..., 32 (AW_RESET_WORDS - 1) are zeroed by the
+// next launch.
 constexpr int AW_FLAG0 = 32;
-constexpr int AW_XCNT = AW_FLAG0 + 8 * 32;
-constexpr int AW_XFLAG0 = AW_XCNT + 32;
-constexpr int AW_SYNC_WORDS = AW_XFLAG0 + 8 * 32;
+constexpr int AW_SYNC_WORDS = AW_FLAG0 + 8 * 32;
 static_assert(AW_SYNC_WORDS == 32 * AW_RESET_WORDS, "every hand-off word is reset");
-// the W1/W3 role (MLP): 2 rows per wave, 4 chunks per step, x in 1 float4 per thread (n <= 4096);
-// AW_MLP_EARLY: its first weight steps are requested before the hand-off (measured: they slow the
-// attention chain by ~3 us at 4k)
-#ifndef AW_MLP_EARLY
-#define AW_MLP_EARLY 0
-#endif
-template <int DT>
-using AwMlpShape = GemvShape<AW_THREADS, 2, 4, true, 4, true, 1, 2>;
-
-__device__ __forceinline__ void aw_poll_xcd_flag(unsigned* sync, const int flag0) {
-    poll_xcd_flag(sync + flag0, sync + 2);
-}
 
 // More than MAXS partials per head to merge (aw_stage_merged keeps MAXS in registers beside
 // the Wo rows): the attention side merges instead (attn_block SIGNAL), so a Wo workgroup
@@ -196,11 +173,10 @@ __device__ __forceinline__ void aw_stage_out(const float* src, const int n, floa
 
 // trace (debug, null = off): per workgroup [8]: start, attention done | hand-off passed, end;
 // attention workgroups also [2] split known, [3] scores done, [4] p.V done, [5] partial drained
-template <int DT, int HD, int QPK, bool MLP = false>
+template <int DT, int HD, int QPK>
 __global__ __launch_bounds__(AW_THREADS) void attn_wo_kernel(const AttnArgs aa, const GemvArgs ga,
                                                                   const int n_kv_heads, unsigned* sync,
-                                                                  unsigned long long* trace, const GemvArgs ma,
-                                                                  const int nb_wo) {
+                                                                  unsigned long long* trace) {
     using S = AwShape<DT>;
     constexpr int E = WDec<DT>::E;
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -234,28 +210,25 @@ __global__ __launch_bounds__(AW_THREADS) void attn_wo_kernel(const AttnArgs aa, 
         if (trace && threadIdx.x == 0) trace[8 * b + 1] = __builtin_amdgcn_s_memrealtime();
         return;
     }
-    if constexpr (MLP) {
-        if (b >= n_att + nb_wo) {
-            // the W1/W3 role: weights requested, then wait for x (all Wo rows published)
-            auto wait_x = [&]() {
-                aw_poll_xcd_flag(sync, AW_XFLAG0);
-                if (trace && threadIdx.x == 0) trace[8 * b + 1] = __builtin_amdgcn_s_memrealtime();
-            };
-            gemv_after<DT, PRO_RMSNORM, EPI_GLU, AwMlpShape<DT>, decltype(wait_x), AW_MLP_EARLY>(
-                ma, b - n_att - nb_wo, gridDim.x - n_att - nb_wo, smem, wait_x);
-            if (trace) {
-                __syncthreads();
-                if (threadIdx.x == 0) trace[8 * b + 2] = __builtin_amdgcn_s_memrealtime();
-            }
-            return;
-        }
-    }
     float4* xs4 = (float4*)(smem + LDS_HEAD_BYTES);
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const int nb = MLP ? nb_wo : gridDim.x - n_att;
+    const int nb = gridDim.x - n_att;
     const int g = (b - n_att) * S::WAVES + wid;
     auto wait_heads = [&]() {
-        aw_poll_xcd_flag(sync, AW_FLAG0);
+        if (threadIdx.x == 0) {
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            int xcc;
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 3)" : "=s"(xcc));
+            const unsigned* flag = sync + AW_FLAG0 + 32 * (xcc & 7);
+            while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
+                __builtin_amdgcn_s_sleep(1);
+                if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {  // 2 s at 100 MHz: flag, go on
+                    __hip_atomic_store(sync + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    break;
+                }
+            }
+        }
+        __syncthreads();
         if (trace && threadIdx.x == 0) trace[8 * b + 1] = __builtin_amdgcn_s_memrealtime();
         if (merged) aw_stage_out<E>(aa.out, ga.n, xs4);
         else aw_stage_merged<E, HD>(aa, ga.n, n_active, xs4, (float*)(smem + LDS_HEAD_BYTES + aw_image_bytes<E>(ga.n)));
@@ -295,34 +268,14 @@ __global__ __launch_bounds__(AW_THREADS) void attn_wo_kernel(const AttnArgs aa, 
             if (lane == 0) {
 #pragma unroll
                 for (int r = 0; r < S::ROWS; r++)  // x += Wo . attn (src/infer.cpp:449-452)
-                    if (g * S::ROWS + r < ga.rows) {
-                        // MLP: read in this launch by the W1/W3 workgroups: write-through
-                        if (MLP) st_sc1_f(ga.out + g * S::ROWS + r, xres[r] + acc[r]);
-                        else ga.out[g * S::ROWS + r] = xres[r] + acc[r];
-                    }
+                    if (g * S::ROWS + r < ga.rows) ga.out[g * S::ROWS + r] = xres[r] + acc[r];
             }
         }
     } else {
-        // (the host fuses the MLP only where the Wo rows take the branch above)
         using G = GemvShape<AW_THREADS, S::ROWS, 4, true, 4, false>;
         wait_heads();
         u32x4 none[G::U][G::ROWS];
         gemv_rows<DT, EPI_RESID, G, false>(ga, g, nb * S::WAVES, lane, xs4, none);
-    }
-    if constexpr (MLP) {
-        // publish x: every store drained, then one arrival per workgroup; the last sets the
-        // per-XCD "x ready" flags
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            const unsigned old = __hip_atomic_fetch_add(sync + AW_XCNT, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (old + 1 == (unsigned)nb_wo) {
-#pragma unroll
-                for (int k = 0; k < 8; k++)
-                    __hip_atomic_store(sync + AW_XFLAG0 + 32 * k, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            if (trace) trace[8 * b + 4] = __builtin_amdgcn_s_memrealtime();
-        }
     }
     if (trace) {
         __syncthreads();
@@ -333,23 +286,12 @@ __global__ __launch_bounds__(AW_THREADS) void attn_wo_kernel(const AttnArgs aa, 
     // workgroup (a round trip on the launch's tail)
 }
 
-// LDS bytes: the larger of the attention tiles (at AW_THREADS), the Wo x image and (MLP) the
-// W1/W3 x image (dim = 0: no MLP role)
+// LDS bytes: the larger of the attention tiles (at AW_THREADS) and the Wo x image
 template <int DT>
 inline size_t attn_wo_smem_bytes(const int hd, const int qpk, const int t_max, const int nsplit, const int q_dim,
-                                 const int n_heads, const int dim = 0) {
+                                 const int n_heads) {
     const size_t att = attn_smem_bytes(hd, qpk, t_max, nsplit, AW_THREADS);
     const size_t wo = LDS_HEAD_BYTES + aw_image_bytes<WDec<DT>::E>(q_dim) + sizeof(float) * (size_t)n_heads * (3 * nsplit + 1);
-    const size_t mlp = dim ? LDS_HEAD_BYTES + aw_image_bytes<WDec<DT>::E>(dim) : 0;
-    const size_t m = att > wo ? att : wo;
-    return m > mlp ? m : mlp;
+    return att > wo ? att : wo;
 }
-// the W1/W3 role fits: plain weights, whole pipelined steps, x in one float4 per thread
-template <int DT>
-inline bool aw_mlp_fits(const int dim) {
-    using S = AwMlpShape<DT>;
-    constexpr int E = WDec<DT>::E;
-    return WScale<DT>::BLOCK == 0 && dim % (64 * E * S::U) == 0 && dim <= 4 * S::XN * S::THREADS;
-}
-
 }  // namespace xalm

@@ -29,12 +29,9 @@ enum { PRO_PLAIN = 0, PRO_RMSNORM = 1 };
 enum { EPI_STORE = 0, EPI_RESID = 1, EPI_QKV = 2, EPI_GLU = 3, EPI_LOGITS = 4 };
 
 constexpr int LDS_HEAD_BYTES = 64;  // block-reduction scratch in front of the x image
-#ifndef GEMV_PRE2
-#define GEMV_PRE2 1  // PIPE-2 PF prologue requests two weight steps (gemv_body)
-#endif
+
 // attn_wo.h hand-off words of a layer that the launch after it zeroes (every 32nd word)
-constexpr int AW_RESET_WORDS = 18;
-constexpr int MLP_RESET_WORDS = 9;  // mlp.h: [0] arrivals, [32 (1 + k)] per-XCD flags
+constexpr int AW_RESET_WORDS = 9;
 
 // Launch shape of one gemv instance.
 template <int THREADS_, int ROWS_, int U_, bool NT_ = true, int MINW_ = 4, bool PF_ = true, int XN_ = 0, int PIPE_ = 1>
@@ -77,7 +74,6 @@ struct GemvArgs {
     unsigned long long* trace;  // debug (null = off): per workgroup [4] start, x staged, rows done
     unsigned long long* cand;   // EPI_LOGITS: [gridDim.x] argmax_key of the workgroup's best logit
     unsigned* aw_reset;         // workgroup 0 zeroes words 0, 32, ..., 32 (AW_RESET_WORDS - 1) (attn_wo.h sync)
-    unsigned* mlp_reset;        // workgroup 0 zeroes words 0, 32, ..., 32 (MLP_RESET_WORDS - 1) (mlp.h sync)
 };
 
 // agent-scope relaxed (sc1: L1-bypassing, write-through) accesses for data handed between
@@ -528,13 +524,11 @@ __device__ __forceinline__ void gemv_rows(const GemvArgs& a, int g, const int to
 // FIRST: the first group's step 0 is already in `pre`.
 // gguf blocks (GQ): every step also loads its chunks' block scales (a second register set),
 // and `pre_d` holds the first step's scales.
-// FIRST2 (with FIRST, no gguf blocks): step 1 is already requested too, in `pre2` (gemv_after).
-template <int DT, int EPI, class S, bool FIRST, bool SC1 = false, bool FIRST2 = false>
+template <int DT, int EPI, class S, bool FIRST, bool SC1 = false>
 __device__ __forceinline__ void gemv_rows_pipe(const GemvArgs& a, const int g0, const int total_waves, const int lane,
                                                const float4* xs4, const u32x4 (&pre)[S::U][S::ROWS],
                                                unsigned long long* best = nullptr,
-                                               const float (*pre_d)[S::ROWS] = nullptr,
-                                               const u32x4 (*pre2)[S::ROWS] = nullptr) {
+                                               const float (*pre_d)[S::ROWS] = nullptr) {
     constexpr int ROWS = S::ROWS, U = S::U;
     constexpr int E = WDec<DT>::E;
     constexpr bool GQ = WScale<DT>::BLOCK > 0;
@@ -570,35 +564,6 @@ __device__ __forceinline__ void gemv_rows_pipe(const GemvArgs& a, const int g0, 
     };
     u32x4 wa[U][ROWS], wb[U][ROWS];
     float da[U][ROWS], db[U][ROWS];  // GQ only (otherwise unused)
-    if constexpr (FIRST2) {
-        static_assert(FIRST && !GQ, "two preloaded steps: plain weights only");
-#pragma unroll
-        for (int u = 0; u < U; u++)
-#pragma unroll
-            for (int r = 0; r < ROWS; r++) {
-                wa[u][r] = pre[u][r];
-                wb[u][r] = pre2[u][r];
-            }
-        // both sets in flight at the top of every iteration; a step past `total` re-reads the
-        // last row (gemv_row_ptr clamps) and is never multiplied
-        int k = 0;
-        for (; k + 3 < total; k += 2) {
-            step(wa, da, k);
-            load(wa, da, k + 2);
-            step(wb, db, k + 1);
-            load(wb, db, k + 3);
-        }
-        if (k + 2 < total) {
-            step(wa, da, k);
-            load(wa, da, k + 2);
-            step(wb, db, k + 1);
-            step(wa, da, k + 2);
-        } else {
-            step(wa, da, k);
-            if (k + 1 < total) step(wb, db, k + 1);
-        }
-        return;
-    }
     if constexpr (FIRST) {
 #pragma unroll
         for (int u = 0; u < U; u++)
@@ -627,24 +592,10 @@ __device__ __forceinline__ void gemv_rows_pipe(const GemvArgs& a, const int g0, 
     }
 }
 
-// Step k of the pipelined stream of the wave whose first group is g0 (gemv_rows_pipe's order):
-// group g0 + (k / steps) * total_waves, chunks from (k % steps) * U.  Steps past the wave's
-// last one re-read the matrix's last row (clamped), unused.
-template <class S, int E>
-__device__ __forceinline__ void pipe_load_step(const GemvArgs& a, const int g0, const int total_waves, const int lane,
-                                               u32x4 (&w)[S::U][S::ROWS], const int k) {
-    const int steps = a.n / (64 * E * S::U);
-    const int q = k / steps;
-    size_t rs;
-    const char* wrow = gemv_row_ptr<S::ROWS>(a, g0 + q * total_waves, lane, rs);
-    gemv_load<S::ROWS, S::U, S::NT>(w, wrow, rs, (k - q * steps) * S::U);
-}
-
 // PF staging, part 1: this thread's x float4s (and norm weights) into registers.  Issued
 // BEFORE the weight prefetch, so waiting for them (vmcnt counts in issue order) leaves the
 // weight chunks in flight.
-// SC1: x was published inside the running launch (write-through): sc1 loads.
-template <int PRO, class S, bool SC1 = false>
+template <int PRO, class S>
 __device__ __forceinline__ void stage_x_issue(const GemvArgs& a, float4 (&xv)[S::XN], float4 (&nw)[S::XN]) {
     const int n4 = a.n >> 2;
     const float4* x4 = (const float4*)a.x;
@@ -653,12 +604,7 @@ __device__ __forceinline__ void stage_x_issue(const GemvArgs& a, float4 (&xv)[S:
 #pragma unroll
     for (int j = 0; j < S::XN; j++) {
         const int i = min((int)threadIdx.x + j * S::THREADS, n4 - 1);
-        if constexpr (SC1) {
-            const u32x4 u = ld_sc1_x4(a.x, (uint32_t)i * 16);
-            xv[j] = make_float4(bits_f32(u.x), bits_f32(u.y), bits_f32(u.z), bits_f32(u.w));
-        } else {
-            xv[j] = x4[i];
-        }
+        xv[j] = x4[i];
         if (PRO != PRO_PLAIN) nw[j] = load_norm4_nb(a.norm_w, a.norm_dtype, a.n, i);
     }
 }
@@ -706,86 +652,9 @@ __device__ __forceinline__ void stage_x_finish(const GemvArgs& a, const float4 (
     }
 }
 
-// Wait (thread 0 polls, then a workgroup barrier) until this workgroup's XCD's flag,
-// flags[32 * xcd], is nonzero: relaxed agent-scope loads with s_sleep (one polled line per XCD
-// instead of every workgroup polling an arrival counter).  2 s bound: sets the sticky *err word
-// and goes on (the host reports it; results are then invalid).
-__device__ __forceinline__ void poll_xcd_flag(const unsigned* flags, unsigned* err) {
-    if (threadIdx.x == 0) {
-        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        int xcc;
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 3)" : "=s"(xcc));
-        const unsigned* flag = flags + 32 * (xcc & 7);
-        while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
-            __builtin_amdgcn_s_sleep(1);
-            if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {  // 2 s at 100 MHz
-                __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                break;
-            }
-        }
-    }
-    __syncthreads();
-}
-// One arrival of this workgroup on *count after its stores drained (write-through stores, so
-// the data is in memory once vmcnt is 0); the arrival that completes `target` sets the 8 per-XCD
-// flags flags[32 k].
-__device__ __forceinline__ void arrive_publish(unsigned* count, const unsigned target, unsigned* flags) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const unsigned old = __hip_atomic_fetch_add(count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (old + 1 == target) {
-#pragma unroll
-            for (int k = 0; k < 8; k++) __hip_atomic_store(flags + 32 * k, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
-}
-
-// One workgroup's share of a gemv whose input x is produced INSIDE the running launch (attn_wo.h
-// with the W1/W3 matvec fused): every wave requests its first two weight steps (the PIPE shape's
-// two register sets), then `wait()` returns once x is published, x is staged with sc1 loads
-// (rmsnorm as the PF prologue), and the pipelined stream continues from the preloaded sets.
-// block / n_blocks: this workgroup's index among the role's workgroups.  Host-checked: PF shape
-// with PIPE 2, plain weights, n % (64 E U) == 0, n <= 4 XN THREADS.
-// EARLY false: the two steps are requested after the wait instead (no weight traffic beside
-// whatever the launch's other roles are doing while they wait).
-template <int DT, int PRO, int EPI, class S, class Wait, bool EARLY = true>
-__device__ __forceinline__ void gemv_after(const GemvArgs& a, const int block, const int n_blocks, char* smem,
-                                           const Wait& wait) {
-    static_assert(S::PF && S::PIPE == 2 && WScale<DT>::BLOCK == 0, "gemv_after: pipelined plain weights");
-    constexpr int E = WDec<DT>::E;
-    float* red = (float*)smem;
-    float4* xs4 = (float4*)(smem + LDS_HEAD_BYTES);
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const int g = block * S::WAVES + wid;
-    const int total_waves = n_blocks * S::WAVES;
-    const int n_groups = gemv_groups<S>(a);
-    const int g0 = min(g, n_groups - 1);  // a wave past the last group re-reads it (unused)
-    u32x4 pre[S::U][S::ROWS], pre2[S::U][S::ROWS];
-    if constexpr (EARLY) {
-        pipe_load_step<S, E>(a, g0, total_waves, lane, pre, 0);
-        pipe_load_step<S, E>(a, g0, total_waves, lane, pre2, 1);
-    }
-    wait();
-    float4 xv[S::XN], nw[S::XN];
-    stage_x_issue<PRO, S, true>(a, xv, nw);
-    if constexpr (!EARLY) {  // behind the x loads, as the PF prologue
-        pipe_load_step<S, E>(a, g0, total_waves, lane, pre, 0);
-        pipe_load_step<S, E>(a, g0, total_waves, lane, pre2, 1);
-    }
-    stage_x_finish<E, PRO, S>(a, xv, nw, xs4, red);
-    __syncthreads();
-    if (g < n_groups) gemv_rows_pipe<DT, EPI, S, true, false, true>(a, g, total_waves, lane, xs4, pre, nullptr, nullptr, pre2);
-}
-
-// Grid: every wave owns the same number of ROWS-row groups (g = wave, wave + W, ...), so no
-// wave is left with a partial last round.  PF shapes (host-checked: n <= 4 * XN * THREADS and
-// n >= 64 * E * U):
-// x (and the norm weights) are requested first, then the first U weight chunks of the wave's
-// first group, so the HBM round trip of the weights overlaps the x prologue.
 // The whole matvec of one workgroup: block / n_blocks are its index and the count among the
-// workgroups that run this matvec (gemv_kernel: block / n_blocks; mlp.h: one role of a
-// fused launch).  SC1: outputs stored write-through (read by another role of the same launch).
+// workgroups that run this matvec (gemv_kernel: blockIdx.x / gridDim.x).  SC1: outputs stored
+// write-through (for a consumer inside the same launch).
 template <int DT, int PRO, int EPI, class S, bool SC1 = false>
 __device__ __forceinline__ void gemv_body(const GemvArgs& a, const int block, const int n_blocks, char* smem) {
     float* red = (float*)smem;
@@ -802,7 +671,6 @@ __device__ __forceinline__ void gemv_body(const GemvArgs& a, const int block, co
         a.trace[4 * block + 3] = ((unsigned long long)xcc << 32) | hw;  // XCD, HW_ID (CU / SE bits)
     }
     if (a.aw_reset && block == 0 && threadIdx.x < AW_RESET_WORDS) a.aw_reset[32 * threadIdx.x] = 0u;
-    if (a.mlp_reset && block == 0 && threadIdx.x < MLP_RESET_WORDS) a.mlp_reset[32 * threadIdx.x] = 0u;
     unsigned long long best = 0;  // EPI_LOGITS: this wave's best candidate (lane 0)
 
     // gguf blocks: the pipelined PF shapes (block scales loaded beside the codes), else staged
@@ -814,16 +682,7 @@ __device__ __forceinline__ void gemv_body(const GemvArgs& a, const int block, co
         const bool prefetched = g < n_groups;
         u32x4 pre[S::U][S::ROWS];
         float pre_d[S::U][S::ROWS];
-        // PIPE 2 with plain weights: both register sets requested inside the prologue (two
-        // steps in flight while x is staged, as after it)
-        constexpr bool PRE2 = S::PIPE == 2 && WScale<DT>::BLOCK == 0 && GEMV_PRE2;
-        u32x4 pre2[S::U][S::ROWS];
-        if constexpr (PRE2) {
-            pipe_load_step<S, E>(a, min(g, n_groups - 1), n_blocks * S::WAVES, lane, pre, 0);
-            pipe_load_step<S, E>(a, min(g, n_groups - 1), n_blocks * S::WAVES, lane, pre2, 1);
-        } else {
-            gemv_prefetch<S>(a, min(g, n_groups - 1), lane, pre);
-        }
+        gemv_prefetch<S>(a, min(g, n_groups - 1), lane, pre);
         if constexpr (WScale<DT>::BLOCK > 0) {
             size_t rs;
             const char* wrow = gemv_row_ptr<S::ROWS>(a, min(g, n_groups - 1), lane, rs);
@@ -833,10 +692,7 @@ __device__ __forceinline__ void gemv_body(const GemvArgs& a, const int block, co
         if (EPI == EPI_QKV && block == 0) rotate_sinks<S::THREADS>(a, a.sp->kv_sink);
         __syncthreads();
         if (a.trace && threadIdx.x == 0) a.trace[4 * block + 1] = __builtin_amdgcn_s_memrealtime();
-        if constexpr (PRE2) {
-            if (prefetched)
-                gemv_rows_pipe<DT, EPI, S, true, SC1, true>(a, g, n_blocks * S::WAVES, lane, xs4, pre, &best, nullptr, pre2);
-        } else if constexpr (S::PIPE == 2) {
+        if constexpr (S::PIPE == 2) {
             if (prefetched) gemv_rows_pipe<DT, EPI, S, true, SC1>(a, g, n_blocks * S::WAVES, lane, xs4, pre, &best, pre_d);
         } else {
             if (prefetched) gemv_rows<DT, EPI, S, true, SC1>(a, g, n_blocks * S::WAVES, lane, xs4, pre, &best);

@@ -112,13 +112,8 @@ struct xh_ctx {
     bool cand_valid = false;        // cand describes the logits on the device
     int dec_cap = 0;
     int nsplit = 1, t_max = 16;
-    // fused attention + Wo launch (attn_wo.h): per-layer hand-off words [n_layers][AW_SYNC_WORDS];
-    // fuse_level 2 also runs the layer's W1/W3 matvec in that launch (where the shapes allow)
+    // fused attention + Wo launch (attn_wo.h): per-layer hand-off words [n_layers][4]
     bool fuse_attn_wo = true;
-    int fuse_level = 1;
-    // XH_OPT_FUSE_MLP: W1/W3 and W2 in one launch (mlp.h); hand-off words [n_layers][MLP_SYNC_WORDS]
-    bool fuse_mlp = false;
-    unsigned* mlp_sync = nullptr;
     unsigned* aw_sync = nullptr;
     // batched prefill (prefill.h), buffers allocated on first use
     bool prefill_batched = true;
@@ -153,15 +148,13 @@ struct xh_ctx {
     // (tools/gemv_bench GB_T1K: 10.95 -> 10.12 us f16, 7.93 -> 7.34 us fp8)
     int qkv_waves = 2048;
     int n_cu = 0;
-    bool balance = false;  // XH_OPT_BALANCE: one workgroup per CU for qkv / W1/W3 (ShapeB12 / B14)
-    // attn_wo.h debug timeline (xh_debug_trace): [workgroup][8] device-clock stamps
+    // debug timelines (xh_debug_trace): device-clock stamps per workgroup
     unsigned long long* aw_trace = nullptr;
     size_t aw_trace_len = 0;
-    bool aw_trace_on = false;
-    bool mlp_trace_on = false;  // fused W1/W3 + W2 launches write aw_trace ([workgroup][4])
-    bool w13_trace_on = false;  // plain W1/W3 launches write aw_trace ([workgroup][4])
-    // the last layer's launches and the lm_head each write their own region of aw_trace
-    // (LT_QKV ...): the step's timeline, kernel boundaries included (tools/layer_trace.py)
+    bool aw_trace_on = false;   // attn_wo launches ([workgroup][8])
+    bool w13_trace_on = false;  // plain W1/W3 launches ([workgroup][4]: tools/balance_trace.py)
+    // the last layer's launches and the lm_head each write their own region (LT_*): the step's
+    // timeline, kernel boundaries included (tools/layer_trace.py)
     bool layer_trace_on = false;
     uint16_t* kcache(int l) { return kv + (size_t)l * 2 * c.max_seq_len * kv_dim; }
     uint16_t* vcache(int l) { return kcache(l) + (size_t)c.max_seq_len * kv_dim; }
@@ -238,14 +231,19 @@ void launch_gemv_s(const GemvArgs& a, hipStream_t s, int max_waves) {
 // 568 -> 584 tok/s (their 4 KiB rows are one step per group, so a wave drained to zero at
 // every group), f16 unchanged (383 / 383); W2, Wo and lm_head unchanged either way
 using ShapePF2P = GemvShape<512, ROWS, UNROLL, true, 4, true, 2, 2>;  // n <= 4096
-// One workgroup per CU with the same row-group count on every CU (the 512-thread grids of qkv
-// and W1/W3 leave CUs with one workgroup idle for the last third of the launch, or unused:
-// tools/balance_trace.py): 12 waves x 1 group (qkv of Mistral / Llama: 3072 groups on 256 CUs),
-// 14 waves x 4 groups (W1/W3: 14336 groups)
-using ShapeB12 = GemvShape<768, ROWS, UNROLL, true, 3, true, 2, 2>;
-using ShapeB14 = GemvShape<896, ROWS, UNROLL, true, 4, true, 2, 2>;
-// CUs to balance over (XH_OPT_BALANCE; 0 = the 512-thread shapes)
-thread_local int g_balance_cu = 0;
+// qkv with 2-byte weights (QKV_T384): 384-thread workgroups, two per CU, every wave ONE row group
+// at 3072 waves (tools/gemv_bench GB_BAL: 10.29 -> 9.95 us f16; fp8 rows are one step: no gain)
+using ShapeQ384 = GemvShape<384, ROWS, UNROLL, true, 3, true, 3, 2>;  // n <= 4608
+#ifndef QKV_T384
+#define QKV_T384 1
+#endif
+// W2-long rows of one-byte weights (W2_T1024): one 1024-thread workgroup per CU, one row per
+// wave, hb in 4 float4 per thread (tools/gemv_bench GB_W2, fp8 Mistral W2: 12.58 -> 11.99 us;
+// f16 no gain)
+using ShapeW2K = GemvShape<1024, 1, UNROLL, true, 4, true, 4, 1>;  // n <= 16384
+#ifndef W2_T1024
+#define W2_T1024 1
+#endif
 
 
 template <int DT, int PRO, int EPI>
@@ -256,15 +254,12 @@ void launch_gemv_t(const GemvArgs& a, hipStream_t s, int max_waves) {
     // PF needs whole first chunks (n >= 64 E U) and x in XN float4 per thread
     const bool pf = !gq_dt(DT) && a.n % 4 == 0 && a.n >= 64 * E * UNROLL;
     if constexpr ((EPI == EPI_QKV || EPI == EPI_GLU) && !gq_dt(DT)) {
-        if (pf && a.n / 4 <= 2 * 512 && a.n % (64 * E * UNROLL) == 0) {
-            const int groups = (a.rows + ROWS - 1) / ROWS, cu = g_balance_cu;
-            if (cu > 0 && groups % cu == 0) {
-                const int gpc = groups / cu;  // row groups per CU
-                if (gpc % 12 == 0 && gpc / 12 <= 8) return launch_gemv_s<DT, PRO, EPI, ShapeB12>(a, s, 12 * cu);
-                if (gpc % 14 == 0 && gpc / 14 <= 8) return launch_gemv_s<DT, PRO, EPI, ShapeB14>(a, s, 14 * cu);
-            }
-            return launch_gemv_s<DT, PRO, EPI, ShapePF2P>(a, s, max_waves);
+        if constexpr (EPI == EPI_QKV && E <= 8 && QKV_T384) {
+            if (pf && a.n / 4 <= 3 * 384 && a.n % (64 * E * UNROLL) == 0)
+                return launch_gemv_s<DT, PRO, EPI, ShapeQ384>(a, s, 3 * (max_waves / 2));
         }
+        if (pf && a.n / 4 <= 2 * 512 && a.n % (64 * E * UNROLL) == 0)
+            return launch_gemv_s<DT, PRO, EPI, ShapePF2P>(a, s, max_waves);
     }
     if constexpr (gq_dt(DT)) {
         // gguf blocks: the pipelined PF shapes with the block scales loaded beside the codes.
@@ -282,7 +277,10 @@ void launch_gemv_t(const GemvArgs& a, hipStream_t s, int max_waves) {
         }
     }
     if (pf && a.n / 4 <= 2 * 512) launch_gemv_s<DT, PRO, EPI, ShapePF2>(a, s, max_waves);
-    else if constexpr (PRO == PRO_PLAIN) {
+    else if constexpr (PRO == PRO_PLAIN && EPI == EPI_RESID && E >= 16 && W2_T1024) {
+        if (pf && a.n / 4 <= 4 * 1024) launch_gemv_s<DT, PRO, EPI, ShapeW2K>(a, s, max_waves);
+        else launch_gemv_s<DT, PRO, EPI, ShapeLong>(a, s, max_waves);
+    } else if constexpr (PRO == PRO_PLAIN) {
         if (pf && a.n / 4 <= 8 * 512) launch_gemv_s<DT, PRO, EPI, ShapePF8>(a, s, max_waves);
         else launch_gemv_s<DT, PRO, EPI, ShapeLong>(a, s, max_waves);
     } else if (gemv_smem_bytes<DT, ShapeShort>(a.n) <= 40 * 1024) {
@@ -377,8 +375,6 @@ GemvArgs qkv_args(xh_ctx* ctx, int l) {
     a.q_dim = ctx->q_dim; a.kv_dim = ctx->kv_dim; a.head_dim = ctx->c.head_dim;
     a.rope_freq = ctx->rope_freq; a.sink_cos = ctx->sink_cos; a.sink_sin = ctx->sink_sin;
     a.qkv_clip = ctx->c.qkv_clip; a.sp = ctx->sp;
-    // the layer's MLP hand-off words start at zero for its fused W1/W3 + W2 launch
-    if (ctx->fuse_mlp) a.mlp_reset = ctx->mlp_sync + (size_t)MLP_SYNC_WORDS * l;
     if (layer_traced(ctx, l)) a.trace = ctx->aw_trace + LT_QKV;
     return a;
 }
@@ -396,7 +392,6 @@ GemvArgs w13_args(xh_ctx* ctx, int l) {
     a.n = ctx->c.dim; a.rows = 2 * ctx->c.hidden_dim; a.x = ctx->x;
     a.norm_w = w.ffn_norm; a.norm_dtype = w.fn_dt; a.eps = ctx->c.norm_eps;
     a.out = ctx->hb; a.act = ctx->c.act; a.sp = ctx->sp;
-    // debug timeline of the plain W1/W3 launch ([workgroup][4]; the fused MLP launch writes its own)
     if (ctx->w13_trace_on) a.trace = ctx->aw_trace;
     if (layer_traced(ctx, l)) a.trace = ctx->aw_trace + LT_W13;
     return a;
@@ -470,63 +465,34 @@ bool use_attn_wo(const xh_ctx* ctx, int l) {
            (dt == XH_F32 || dt == XH_F16 || dt == XH_BF16 || dt == XH_F8_E4M3 || dt == XH_F8_E5M2 || dt == XH_Q8);
 }
 
-// mlp: the layer's W1/W3 matvec joins the launch (XH_E_INVALID, nothing launched, where the
-// shapes do not allow it)
-int launch_attn_wo(xh_ctx* ctx, int l, hipStream_t s, bool mlp = false) {
+int launch_attn_wo(xh_ctx* ctx, int l, hipStream_t s) {
     const AttnArgs aa = attn_args(ctx, l);
     const GemvArgs ga = wo_args(ctx, l);
-    const GemvArgs m13 = w13_args(ctx, l);
-    const GemvArgs* ma = mlp ? &m13 : nullptr;
     unsigned* sync = ctx->aw_sync + (size_t)AW_SYNC_WORDS * l;
     const int hd = ctx->c.head_dim, qpk = ctx->qpk, nkv = ctx->c.n_kv_heads, tm = ctx->t_max_aw;
     const int mw = ctx->max_gemv_waves;
     unsigned long long* tr = ctx->aw_trace_on ? ctx->aw_trace : layer_traced(ctx, l) ? ctx->aw_trace + LT_AW : nullptr;
     switch (ctx->L[l].wo_dt) {
-        case XH_F32: return aw_launch_dt1(aa, ga, ma, hd, qpk, nkv, tm, sync, mw, s, tr);
-        case XH_F16: return aw_launch_dt2(aa, ga, ma, hd, qpk, nkv, tm, sync, mw, s, tr);
-        case XH_BF16: return aw_launch_dt3(aa, ga, ma, hd, qpk, nkv, tm, sync, mw, s, tr);
-        case XH_F8_E4M3: return aw_launch_dt6(aa, ga, ma, hd, qpk, nkv, tm, sync, mw, s, tr);
-        case XH_F8_E5M2: return aw_launch_dt7(aa, ga, ma, hd, qpk, nkv, tm, sync, mw, s, tr);
-        case XH_Q8: return aw_launch_dt9(aa, ga, ma, hd, qpk, nkv, tm, sync, mw, s, tr);
+        case XH_F32: return aw_launch_dt1(aa, ga, hd, qpk, nkv, tm, sync, mw, s, tr);
+        case XH_F16: return aw_launch_dt2(aa, ga, hd, qpk, nkv, tm, sync, mw, s, tr);
+        case XH_BF16: return aw_launch_dt3(aa, ga, hd, qpk, nkv, tm, sync, mw, s, tr);
+        case XH_F8_E4M3: return aw_launch_dt6(aa, ga, hd, qpk, nkv, tm, sync, mw, s, tr);
+        case XH_F8_E5M2: return aw_launch_dt7(aa, ga, hd, qpk, nkv, tm, sync, mw, s, tr);
+        case XH_Q8: return aw_launch_dt9(aa, ga, hd, qpk, nkv, tm, sync, mw, s, tr);
         default: return XH_E_INVALID;
     }
-}
-// W1/W3 + W2 of layer l in one launch (mlp.h): XH_E_INVALID (nothing launched) where the shapes
-// do not fit.  a13 carries the attn_wo hand-off reset of the layer.
-int launch_mlp(xh_ctx* ctx, int l, const GemvArgs& a13, hipStream_t s) {
-    const LayerW& w = ctx->L[l];
-    if (!ctx->fuse_mlp || w.w13_dt != w.w2_dt || w.w13_x || w.w2_x) return XH_E_INVALID;
-    const GemvArgs a2 = w2_args(ctx, l);
-    unsigned* sync = ctx->mlp_sync + (size_t)MLP_SYNC_WORDS * l;
-    unsigned* err = ctx->aw_sync + (size_t)AW_SYNC_WORDS * l + 2;  // the layer's sticky timeout word
-    unsigned long long* tr = ctx->mlp_trace_on ? ctx->aw_trace : nullptr;
-    switch (w.w13_dt) {
-        case XH_F32: return mlp_launch_dt1(a13, a2, sync, err, s, tr);
-        case XH_F16: return mlp_launch_dt2(a13, a2, sync, err, s, tr);
-        case XH_BF16: return mlp_launch_dt3(a13, a2, sync, err, s, tr);
-        case XH_F8_E4M3: return mlp_launch_dt6(a13, a2, sync, err, s, tr);
-        case XH_F8_E5M2: return mlp_launch_dt7(a13, a2, sync, err, s, tr);
-        case XH_Q8: return mlp_launch_dt9(a13, a2, sync, err, s, tr);
-        default: return XH_E_INVALID;
-    }
-}
-
-// fuse level 2 for layer l: W1/W3 shares Wo's dtype and decode form (one instantiation)
-bool use_aw_mlp(const xh_ctx* ctx, int l) {
-    const LayerW& w = ctx->L[l];
-    return ctx->fuse_level >= 2 && use_attn_wo(ctx, l) && w.w13_dt == w.wo_dt && !w.w13_x;
 }
 
 // a fused hand-off that timed out leaves its sticky flag: report it (after the stream sync)
 int check_aw(xh_ctx* ctx) {
-    if (!ctx->fuse_attn_wo && !ctx->fuse_mlp) return 0;
+    if (!ctx->fuse_attn_wo) return 0;
     std::vector<unsigned> h((size_t)ctx->c.n_layers * AW_SYNC_WORDS);
     HIP_TRY(ctx, copy_sync(ctx, h.data(), ctx->aw_sync, h.size() * sizeof(unsigned), hipMemcpyDeviceToHost));
     for (int l = 0; l < ctx->c.n_layers; l++)
         if (h[(size_t)AW_SYNC_WORDS * l + 2]) {
             // reported once: the sticky words are cleared so the context can be reset and reused
             HIP_TRY(ctx, fill_sync(ctx, ctx->aw_sync, 0, h.size() * sizeof(unsigned)));
-            return set_err(ctx, XH_E_HIP, "layer %d: an in-launch hand-off (attention -> Wo -> W1/W3 -> W2) timed out", l);
+            return set_err(ctx, XH_E_HIP, "layer %d: attention -> Wo hand-off timed out", l);
         }
     return 0;
 }
@@ -534,7 +500,6 @@ int check_aw(xh_ctx* ctx) {
 // greedy: the token is the argmax of the previous step's logits (argmax_embed_kernel)
 int enqueue_step(xh_ctx* ctx, hipStream_t s, bool with_logits, bool greedy = false) {
     const xh_config& c = ctx->c;
-    g_balance_cu = ctx->balance ? ctx->n_cu : 0;
     const int mb = ctx->max_gemv_waves;
     if (greedy)
         hipLaunchKernelGGL(argmax_embed_kernel, dim3(1), dim3(ARGMAX_CANDS), 0, s, (const unsigned long long*)ctx->cand,
@@ -548,19 +513,6 @@ int enqueue_step(xh_ctx* ctx, hipStream_t s, bool with_logits, bool greedy = fal
         if (!launch_gemv<PRO_RMSNORM, EPI_QKV>(kdt(w.qkv_dt, w.qkv_x), qkv_args(ctx, l), s, qkv_launch_waves(ctx, l)))
             return set_err(ctx, XH_E_INVALID, "layer %d: unsupported qkv dtype %d", l, w.qkv_dt);
         GemvArgs a13 = w13_args(ctx, l);
-        if (use_aw_mlp(ctx, l)) {
-            const int rc = launch_attn_wo(ctx, l, s, true);
-            if (rc == 0) {
-                // W2 right behind it zeroes the hand-off words for the next step
-                GemvArgs a2 = w2_args(ctx, l);
-                a2.aw_reset = ctx->aw_sync + (size_t)AW_SYNC_WORDS * l;
-                if (!launch_gemv<PRO_PLAIN, EPI_RESID>(kdt(w.w2_dt, w.w2_x), a2, s, mb))
-                    return set_err(ctx, XH_E_INVALID, "layer %d: unsupported w2 dtype", l);
-                continue;
-            }
-            if (rc != XH_E_INVALID) return set_err(ctx, rc, "layer %d: fused attention + Wo + W1/W3 launch failed", l);
-            // the shapes do not take the W1/W3 role: level 1 for this layer
-        }
         if (use_attn_wo(ctx, l)) {
             const int rc = launch_attn_wo(ctx, l, s);
             if (rc) return set_err(ctx, rc, "layer %d: fused attention + Wo launch failed", l);
@@ -571,11 +523,6 @@ int enqueue_step(xh_ctx* ctx, hipStream_t s, bool with_logits, bool greedy = fal
                 return set_err(ctx, XH_E_INVALID, "unsupported head_dim %d / q-per-kv %d", c.head_dim, ctx->qpk);
             if (!launch_gemv<PRO_PLAIN, EPI_RESID>(kdt(w.wo_dt, w.wo_x), wo_args(ctx, l), s, mb))
                 return set_err(ctx, XH_E_INVALID, "layer %d: unsupported wo dtype", l);
-        }
-        {
-            const int rc = launch_mlp(ctx, l, a13, s);
-            if (rc == 0) continue;
-            if (rc != XH_E_INVALID) return set_err(ctx, rc, "layer %d: fused W1/W3 + W2 launch failed", l);
         }
         if (!launch_gemv<PRO_RMSNORM, EPI_GLU>(kdt(w.w13_dt, w.w13_x), a13, s, mb))
             return set_err(ctx, XH_E_INVALID, "layer %d: unsupported w1/w3 dtype", l);
@@ -1044,7 +991,6 @@ int xh_create(const xh_config* cfg, int device_ordinal, xh_ctx** out) {
     CREATE_TRY(dmalloc(ctx, &ctx->part_ml, (size_t)ctx->nsplit * c.n_heads * 2));
     CREATE_TRY(dmalloc(ctx, &ctx->attn_cnt, (size_t)c.n_kv_heads));
     CREATE_TRY(dmalloc(ctx, &ctx->aw_sync, (size_t)c.n_layers * AW_SYNC_WORDS));
-    CREATE_TRY(dmalloc(ctx, &ctx->mlp_sync, (size_t)c.n_layers * MLP_SYNC_WORDS));
     CREATE_TRY(dmalloc(ctx, &ctx->cand, (size_t)ARGMAX_CANDS));
     CREATE_TRY(dmalloc(ctx, &ctx->scan_flag, (size_t)1));
     {
@@ -1104,7 +1050,7 @@ void xh_destroy(xh_ctx* ctx) {
     if (ctx->wcls && ctx->wcls != ctx->embed) hipFree(ctx->wcls);
     hipFree(ctx->embed); hipFree(ctx->final_norm);
     hipFree(ctx->kv); hipFree(ctx->x); hipFree(ctx->q); hipFree(ctx->attn_out); hipFree(ctx->hb);
-    hipFree(ctx->logits); hipFree(ctx->part_o); hipFree(ctx->part_ml); hipFree(ctx->attn_cnt); hipFree(ctx->aw_sync); hipFree(ctx->mlp_sync); hipFree(ctx->cand); hipFree(ctx->scan_flag);
+    hipFree(ctx->logits); hipFree(ctx->part_o); hipFree(ctx->part_ml); hipFree(ctx->attn_cnt); hipFree(ctx->aw_sync); hipFree(ctx->cand); hipFree(ctx->scan_flag);
     hipFree(ctx->pf_tok); hipFree(ctx->pf_x); hipFree(ctx->pf_xn); hipFree(ctx->pf_q); hipFree(ctx->pf_att); hipFree(ctx->pf_h);
     hipFree(ctx->pf_xh); hipFree(ctx->pf_xl); hipFree(ctx->pf_xs);
     hipFree(ctx->pf_logits); hipFree(ctx->pf_tgt); hipFree(ctx->ppl_tgt); hipFree(ctx->ppl_prob);
@@ -1508,7 +1454,6 @@ int xh_reset(xh_ctx* ctx) {
     // the attention + Wo hand-off words (normally zeroed by each layer's W1/W3 launch): a step
     // that failed between the two launches must not leave a stale arrival count
     HIP_TRY(ctx, hipMemsetAsync(ctx->aw_sync, 0, (size_t)c.n_layers * AW_SYNC_WORDS * 4, ctx->stream));
-    HIP_TRY(ctx, hipMemsetAsync(ctx->mlp_sync, 0, (size_t)c.n_layers * MLP_SYNC_WORDS * 4, ctx->stream));
     HIP_TRY(ctx, hipMemsetAsync(ctx->cand, 0, ARGMAX_CANDS * 8, ctx->stream));
     ctx->cand_valid = true;  // all-zero candidates = zero logits (argmax token 0)
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
@@ -1631,7 +1576,6 @@ int xh_debug_trace(xh_ctx* ctx, int enable, uint64_t* out, int cap, int* len) {
     }
     if (enable >= 0) {
         ctx->aw_trace_on = (enable & 2) != 0;
-        ctx->mlp_trace_on = (enable & 4) != 0;
         ctx->w13_trace_on = (enable & 8) != 0;
         ctx->layer_trace_on = (enable & 16) != 0 && ctx->aw_trace_len >= LT_WORDS;
         drop_graphs(ctx);
@@ -1643,11 +1587,9 @@ int xh_debug_trace(xh_ctx* ctx, int enable, uint64_t* out, int cap, int* len) {
 int xh_get_option(const xh_ctx* ctx, int option, int* value) {
     if (!ctx || !value) return XH_E_INVALID;
     switch (option) {
-        case XH_OPT_FUSE_ATTN_WO: *value = ctx->fuse_attn_wo ? ctx->fuse_level : 0; return 0;
+        case XH_OPT_FUSE_ATTN_WO: *value = ctx->fuse_attn_wo ? 1 : 0; return 0;
         case XH_OPT_PREFILL: *value = ctx->prefill_batched ? ctx->prefill_gemm : 0; return 0;
         case XH_OPT_PREFILL_GLU_SPLIT: *value = ctx->pf_glu_split ? 1 : 0; return 0;
-        case XH_OPT_FUSE_MLP: *value = ctx->fuse_mlp ? 1 : 0; return 0;
-        case XH_OPT_BALANCE: *value = ctx->balance ? 1 : 0; return 0;
         default: return XH_E_INVALID;
     }
 }
@@ -1656,25 +1598,14 @@ int xh_set_option(xh_ctx* ctx, int option, int value) {
     if (!ctx) return XH_E_INVALID;
     switch (option) {
         case XH_OPT_FUSE_ATTN_WO:
-            if (value < 0 || value > 2) return set_err(ctx, XH_E_INVALID, "fuse level %d not in 0..2", value);
+            if (value < 0 || value > 1) return set_err(ctx, XH_E_INVALID, "fuse level %d not in 0..1", value);
             ctx->fuse_attn_wo = value != 0;
-            ctx->fuse_level = value;
             drop_graphs(ctx);
             return 0;
         case XH_OPT_PREFILL:
             if (value < 0 || value > 3) return set_err(ctx, XH_E_INVALID, "XH_OPT_PREFILL: 0 ... 3");
             ctx->prefill_batched = value != 0;
             if (value) ctx->prefill_gemm = value;
-            return 0;
-        case XH_OPT_BALANCE:
-            if (value < 0 || value > 1) return set_err(ctx, XH_E_INVALID, "XH_OPT_BALANCE: 0 or 1");
-            ctx->balance = value != 0;
-            drop_graphs(ctx);
-            return 0;
-        case XH_OPT_FUSE_MLP:
-            if (value < 0 || value > 1) return set_err(ctx, XH_E_INVALID, "XH_OPT_FUSE_MLP: 0 or 1");
-            ctx->fuse_mlp = value != 0;
-            drop_graphs(ctx);
             return 0;
         case XH_OPT_PREFILL_GLU_SPLIT:
             if (value < 0 || value > 1) return set_err(ctx, XH_E_INVALID, "XH_OPT_PREFILL_GLU_SPLIT: 0 or 1");
@@ -1800,14 +1731,11 @@ int xh_op_mha(float* xout, const uint16_t* kb, const uint16_t* vb, const float* 
 // timing hooks for bench.py
 // ---------------------------------------------------------------------------------------
 int xh_time_kernel(xh_ctx* ctx, int which, int iters, float* avg_us) {
-    if (!ctx || !avg_us || iters <= 0 || which < 0 || which > 6) return XH_E_INVALID;
-    if (which == 6 && !use_aw_mlp(ctx, 0))
-        return set_err(ctx, XH_E_INVALID, "the attention + Wo + W1/W3 launch needs fuse level 2 and matching dtypes");
+    if (!ctx || !avg_us || iters <= 0 || which < 0 || which > 5) return XH_E_INVALID;
     HIP_TRY(ctx, hipSetDevice(ctx->dev));
     int rc = check_ready(ctx);
     if (rc) return rc;
     const int mb = ctx->max_gemv_waves;
-    g_balance_cu = ctx->balance ? ctx->n_cu : 0;
     // launches rotate over the layers, so a repeat never finds its weights in the 256 MB
     // Infinity Cache (a decode step streams every layer once)
     int rot = 0;
@@ -1820,14 +1748,6 @@ int xh_time_kernel(xh_ctx* ctx, int which, int iters, float* avg_us) {
             case 2: return launch_gemv<PRO_PLAIN, EPI_RESID>(kdt(ctx->L[l].wo_dt, ctx->L[l].wo_x), wo_args(ctx, l), ctx->stream, mb);
             case 3: return launch_gemv<PRO_PLAIN, EPI_RESID>(kdt(ctx->L[l].w2_dt, ctx->L[l].w2_x), w2_args(ctx, l), ctx->stream, mb);
             case 4: return launch_gemv<PRO_RMSNORM, EPI_LOGITS>(kdt(ctx->wcls_dt, ctx->wcls_x), cls_args(ctx), ctx->stream, mb);
-            case 6: {
-                // attention + Wo + W1/W3 of layer l, then its W2 (which zeroes the hand-off words,
-                // as in the step): time the pair; the caller subtracts W2 alone (which 3)
-                if (launch_attn_wo(ctx, l, ctx->stream, true)) return false;
-                GemvArgs a2 = w2_args(ctx, l);
-                a2.aw_reset = ctx->aw_sync + (size_t)AW_SYNC_WORDS * l;
-                return launch_gemv<PRO_PLAIN, EPI_RESID>(kdt(ctx->L[l].w2_dt, ctx->L[l].w2_x), a2, ctx->stream, mb);
-            }
             default:
                 return launch_attn(attn_args(ctx, l), ctx->c.head_dim, ctx->qpk, ctx->c.n_kv_heads, ctx->t_max,
                                    ctx->stream);
@@ -1864,10 +1784,6 @@ size_t xh_kernel_bytes(const xh_ctx* ctx, int which, int kv_len) {
         case 3: return (size_t)c.dim * file_row_bytes(w.w2_dt, c.hidden_dim) + c.hidden_dim * vec + 2 * c.dim * vec;
         case 4: return (size_t)c.vocab_size * file_row_bytes(ctx->wcls ? ctx->wcls_dt : ctx->embed_dt, c.dim) +
                        c.dim * (vec + dtype_size(ctx->final_norm_dt)) + (size_t)c.vocab_size * vec;
-        case 6:  // attention + Wo + W1/W3: K/V history, Wo, W1/W3 rows, q, x in/out, hb out
-            return (size_t)2 * kv_len * ctx->kv_dim * 2 + (size_t)c.dim * file_row_bytes(w.wo_dt, ctx->q_dim) +
-                   (size_t)2 * c.hidden_dim * file_row_bytes(w.w13_dt, c.dim) + (size_t)ctx->q_dim * vec +
-                   2 * c.dim * vec + c.dim * dtype_size(w.fn_dt) + (size_t)c.hidden_dim * vec;
         default: return (size_t)2 * kv_len * ctx->kv_dim * 2 + 2 * (size_t)ctx->q_dim * vec;
     }
 }
