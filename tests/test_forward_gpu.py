@@ -1,13 +1,15 @@
 """Whole-forward parity: Model.forward on the HIP path vs the CPU oracle (and HF goldens).
 
 Fixtures are .xalm files written by the reference's convert.py (tests/golden/).
-Tolerance (the north-star bar): logits within 1e-3 max-abs of the CPU path on identical
-token ids; for the head_dim-128 fixture, whose logits reach |87|, the bar is stated
-relative: max-abs <= 1e-3 * max(1, max|logit|) ... in practice both are far below.
+Bars (tests/bars.py): on the fixtures 8x the measured GPU-vs-oracle envelope of that fixture
+and path (tests/golden/error_envelope.json), capped by the north-star bar, 1e-3 max-abs stated
+relative to the logit scale above 1 (small_llama's logits reach |93|); on synthetic models the
+north-star bar.
 """
 import numpy as np
 import pytest
 
+from bars import bar, check, check_logp
 from conftest import fixture_path
 from oracle import oracle as O
 from xalm_amd import _lib as L
@@ -31,10 +33,6 @@ def configure(gm, engine):
     assert gm.get_option(L.OPT_FUSE_ATTN_WO) == FUSE[engine]
 
 
-def tol(ref):
-    return 1e-3 * max(1.0, float(np.abs(ref).max()))
-
-
 def run_pair(name, tokens, context=0, graphs=True, modes=None, engine="graph"):
     xf = XalmFile(fixture_path(name + ".xalm"))
     gm = Model.from_xalm(xf, context=context)
@@ -49,9 +47,8 @@ def run_pair(name, tokens, context=0, graphs=True, modes=None, engine="graph"):
         om.forward(tok, pos, mode)
         if mode == L.OUTPUT_LOGITS:
             ref = om.logits()
-            err = float(np.abs(st.logits() - ref).max())
-            assert err <= tol(ref), (name, pos, err)
-            worst = max(worst, err / tol(ref))
+            err = check(st.logits(), ref, name, "loop", pos)
+            worst = max(worst, err / bar(ref, name))
     return gm, om, worst
 
 
@@ -132,7 +129,8 @@ def test_prefill_matches_oracle(name, context, engine):
     gm.prefill(toks, 0, st)
     for pos, tok in enumerate(toks):
         om.forward(tok, pos, L.OUTPUT_LOGITS if pos == len(toks) - 1 else L.HYDRATE_KV_CACHE)
-    assert np.abs(st.logits() - om.logits()).max() <= tol(om.logits())
+    # a prompt that wraps the ring takes the token loop
+    check(st.logits(), om.logits(), name, "prefill" if len(toks) <= gm.config.max_seq_len else "loop")
     n = min(len(toks), gm.config.max_seq_len)
     for layer in range(gm.config.n_layers):
         a = gm.kv_read(layer, 1, 0, n).view(np.float16).astype(np.float32)
@@ -159,7 +157,7 @@ def test_batched_prefill_matches_oracle(name, n, mode):
     gm.prefill(toks, 0, st)
     for pos, tok in enumerate(toks):
         om.forward(tok, pos, L.OUTPUT_LOGITS if pos == len(toks) - 1 else L.HYDRATE_KV_CACHE)
-    assert np.abs(st.logits() - om.logits()).max() <= tol(om.logits())
+    check(st.logits(), om.logits(), name, "prefill")
     for layer in range(gm.config.n_layers):
         for which in (0, 1):
             a = gm.kv_read(layer, which, 0, n).view(np.float16).astype(np.float32)
@@ -169,7 +167,7 @@ def test_batched_prefill_matches_oracle(name, n, mode):
     gm.get_logits(st)
     for i, t in enumerate(nxt):
         om.forward(t, n + i)
-    assert np.abs(st.logits() - om.logits()).max() <= tol(om.logits())
+    check(st.logits(), om.logits(), name, "prefill")
 
 
 def synthetic_pair(wdt, dim=256, hidden=512, n_layers=2, vocab=512, context=256):
@@ -214,7 +212,7 @@ def test_prefill_gemm_paths_on_synthetic_weights(wdt, mode, glu):
         om.forward(tok, pos, L.OUTPUT_LOGITS if pos == len(toks) - 1 else L.HYDRATE_KV_CACHE)
     ref = om.logits()
     assert np.isfinite(st.logits()).all()
-    assert np.abs(st.logits() - ref).max() <= tol(ref), float(np.abs(st.logits() - ref).max())
+    check(st.logits(), ref)
     gm2, om2 = synthetic_pair(wdt)
     gm2.set_option(L.OPT_PREFILL, mode)
     gm2.set_option(L.OPT_PREFILL_GLU_SPLIT, glu)
@@ -232,12 +230,12 @@ def test_pipelined_gemv_decode(wdt):
     for pos, tok in enumerate(toks):
         gm.forward(st, tok, pos, L.OUTPUT_LOGITS)
         om.forward(tok, pos)
-        assert np.abs(st.logits() - om.logits()).max() <= tol(om.logits()), pos
+        check(st.logits(), om.logits(), what=pos)
     nxt = gm.decode_greedy(len(toks), 3)
     gm.get_logits(st)
     for i, t in enumerate(nxt):
         om.forward(t, len(toks) + i)
-    assert np.abs(st.logits() - om.logits()).max() <= tol(om.logits())
+    check(st.logits(), om.logits())
 
 
 @pytest.mark.parametrize("wdt", [L.F8_E4M3, L.F8_E5M2, L.F16])
@@ -250,7 +248,7 @@ def test_long_row_w2_decode(wdt):
     for pos, tok in enumerate([1, 17, 300, 5]):
         gm.forward(st, tok, pos, L.OUTPUT_LOGITS)
         om.forward(tok, pos)
-        assert np.abs(st.logits() - om.logits()).max() <= tol(om.logits()), pos
+        check(st.logits(), om.logits(), what=pos)
 
 
 @pytest.mark.parametrize("wdt", [L.F16, L.F8_E4M3])
@@ -282,7 +280,7 @@ def test_batched_prefill_equals_token_loop(batched):
         gm.prefill(toks, 0, st)
         out.append((st.logits().copy(), gm.kv_read(1, 0, 0, len(toks)).view(np.float16).astype(np.float32)))
         gm.close()
-    assert np.abs(out[0][0] - out[1][0]).max() <= tol(out[1][0])
+    check(out[0][0], out[1][0], "small_llama_f16", "prefill")
     assert np.abs(out[0][1] - out[1][1]).max() <= 2e-3 * max(1.0, np.abs(out[1][1]).max())
 
 
@@ -302,7 +300,7 @@ def test_engines_agree_on_long_decode():
         gm.close()
     for toks, lg in res[1:]:
         assert toks == res[0][0]
-        assert np.abs(lg - res[0][1]).max() <= tol(res[0][1])
+        check(lg, res[0][1], "small_llama_f16", "loop")
 
 
 def test_graphs_and_eager_bitwise_equal():
@@ -341,7 +339,7 @@ def test_device_greedy_decode_matches_oracle_teacher_forced(engine):
         om.forward(t, pos)
         pos += 1
     gm.get_logits(st)
-    assert np.abs(st.logits() - om.logits()).max() <= tol(om.logits())
+    check(st.logits(), om.logits(), "tiny_mistral_f16", "loop")
 
 
 @pytest.mark.parametrize("engine", ENGINES)
@@ -372,11 +370,12 @@ def test_upload_validation():
         gm.forward(st, 1, 0)  # weights missing
 
 
-def check_probs(got, om, toks):
+def check_probs(got, om, toks, fixture=None):
     """got[i] vs the oracle's Sampler::sample_prob(toks[i+1]) after forwarding toks[i] (the
-    run_perplexity loop, src/main.cpp:243-254).  Bar: |log p - log p_ref| <= 2 x the logits
-    bar of that position (log p moves by at most twice the worst logit error); probabilities
-    the reference underflows to 0 (|logits| ~ 87 on small_llama) must be below 1e-30 here."""
+    run_perplexity loop, src/main.cpp:243-254).  Bar on |log p - log p_ref|: 2 x the logits bar
+    of that position (log p moves by at most twice the worst logit error; path "ppl" of the
+    fixture's envelope); probabilities the reference underflows to 0 (|logits| ~ 90 on
+    small_llama) must be below 1e-30 here."""
     assert got.shape == (len(toks) - 1,)
     for pos in range(len(toks) - 1):
         om.forward(toks[pos], pos)
@@ -386,8 +385,7 @@ def check_probs(got, om, toks):
             assert got[pos] < 1e-30, (pos, got[pos], ref)
             continue
         assert got[pos] > 0, (pos, got[pos], ref)
-        err = abs(np.log(got[pos]) - np.log(ref))
-        assert err <= 2 * tol(lg) + 1e-5, (pos, got[pos], ref, err)
+        check_logp(float(abs(np.log(got[pos]) - np.log(ref))), lg, fixture, pos)
 
 
 @pytest.mark.parametrize("prefill", [1, 2, 3, 0])
@@ -401,7 +399,7 @@ def test_perplexity_probs_match_oracle(name, prefill):
     gm.set_option(L.OPT_PREFILL, prefill)
     om = O.OracleModel.from_xalm(xf, context=256)
     toks = [1] + [3 + (i * 41) % 280 for i in range(89)]
-    check_probs(gm.token_probs(toks), om, toks)
+    check_probs(gm.token_probs(toks), om, toks, name)
 
 
 def test_perplexity_token_loop_ring():
@@ -411,7 +409,7 @@ def test_perplexity_token_loop_ring():
     gm = Model.from_xalm(xf, context=ctxlen)
     om = O.OracleModel.from_xalm(xf, context=ctxlen)
     toks = [1] + [3 + (i * 23) % 290 for i in range(40)]
-    check_probs(gm.token_probs(toks), om, toks)
+    check_probs(gm.token_probs(toks), om, toks, "tiny_mistral_f16")
 
 
 def test_prefill_option_values():
@@ -520,13 +518,13 @@ def test_multi_split_attention_in_model(engine):
     gm.prefill(toks, 0, st)
     for pos, tok in enumerate(toks):
         om.forward(tok, pos, L.OUTPUT_LOGITS if pos == len(toks) - 1 else L.HYDRATE_KV_CACHE)
-    assert np.abs(st.logits() - om.logits()).max() <= tol(om.logits())
+    check(st.logits(), om.logits(), "small_llama_f16", "prefill")
     nxt = gm.decode_greedy(len(toks), 4)
     assert len(nxt) == 4
     gm.get_logits(st)
     for i, t in enumerate(nxt):
         om.forward(t, len(toks) + i)
-    assert np.abs(st.logits() - om.logits()).max() <= tol(om.logits())
+    check(st.logits(), om.logits(), "small_llama_f16", "prefill")
 
 
 @pytest.mark.parametrize("engine", ENGINES)
@@ -557,7 +555,6 @@ def test_long_context_streaming_attention(engine, history):
     st = InferenceState(c)
     gm.forward(st, 17, history, L.OUTPUT_LOGITS)
     om.forward(17, history, L.OUTPUT_LOGITS)
-    ref = om.logits()
-    assert np.abs(st.logits() - ref).max() <= tol(ref)
+    check(st.logits(), om.logits())
     gm.close()
     om.close()

@@ -9,6 +9,7 @@ import numpy as np
 import pytest
 
 import bench
+from bars import check
 from conftest import fixture_path
 from oracle import oracle as O
 from xalm_amd import _lib as L
@@ -32,7 +33,7 @@ def dequant(dtype, w):
     return (d * q).reshape(w.shape[0], -1)
 
 
-def tol(ref):
+def tol(ref):  # the north-star bar (synthetic block models); fixtures: bars.check
     return 1e-3 * max(1.0, float(np.abs(ref).max()))
 
 
@@ -63,15 +64,14 @@ def test_forward_on_converter_blocks(name, fuse):
     for pos, tok in enumerate(toks):
         gm.forward(st, tok, pos)
         om.forward(tok, pos)
-        ref = om.logits()
-        assert np.abs(st.logits() - ref).max() <= tol(ref), (name, pos)
+        check(st.logits(), om.logits(), name, "loop", pos)
     # prompt path (token loop) and the device greedy loop
     gm.reset()
     om.reset()
     gm.prefill(toks[:9], 0, st)
     for pos, tok in enumerate(toks[:9]):
         om.forward(tok, pos, L.OUTPUT_LOGITS if pos == 8 else L.HYDRATE_KV_CACHE)
-    assert np.abs(st.logits() - om.logits()).max() <= tol(om.logits())
+    check(st.logits(), om.logits(), name, "loop")
     out = gm.decode_greedy(9, 6)
     pos = 9
     for t in out:

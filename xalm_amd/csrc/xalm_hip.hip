@@ -970,7 +970,6 @@ int xh_create(const xh_config* cfg, int device_ordinal, xh_ctx** out) {
     ctx->q_dim = c.n_heads * c.head_dim;
     ctx->kv_dim = c.n_kv_heads * c.head_dim;
     ctx->qpk = qpk;
-    if (const char* qw = getenv("XALM_QKV_WAVES")) ctx->qkv_waves = std::max(64, atoi(qw));  // launch-shape sweeps
     ctx->nsplit = attn_nsplit(c.n_kv_heads, c.max_seq_len);
     ctx->t_max = attn_split_len(c.max_seq_len, ctx->nsplit);
     ctx->t_max_aw = attn_split_len(c.max_seq_len, ctx->nsplit, attn_min_t_partials(c.head_dim, AW_THREADS));
