@@ -277,10 +277,10 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--kernel-iters", type=int, default=200)
     ap.add_argument("--prefill-mode", type=int, default=1, choices=(1, 2, 3),
-                    help="batched prefill GEMMs (XH_OPT_PREFILL): 1 default per dtype, 2 split-f16 MFMA "
-                         "wherever the weights allow, 3 f32-input MFMA only")
-    ap.add_argument("--prefill-tokens", type=int, default=512,
-                    help="also time xh_prefill of this many prompt tokens (batched f32-MFMA path; 0 = skip)")
+                    help="batched prefill GEMMs (XH_OPT_PREFILL): 1 default per dtype (hipBLASLt for f16 / "
+                         "e4m3 weights), 2 split-f16 MFMA wherever the weights allow, 3 f32-input MFMA only")
+    ap.add_argument("--prefill-tokens", type=int, default=2048,
+                    help="also time xh_prefill of this many prompt tokens (batched path; 0 = skip)")
     ap.add_argument("--fuse-attn-wo", type=int, default=1, choices=(0, 1),
                     help="attention + Wo in one launch (1) or two launches (0)")
     args = ap.parse_args()
@@ -350,7 +350,7 @@ def main():
     if args.prefill_tokens and batched_ok and not w["kv_prefill"] and args.prefill_tokens <= c.max_seq_len:
         ptoks = prompt_tokens(c.vocab_size, n=args.prefill_tokens, seed=11)
         model.set_option(L.OPT_PREFILL, args.prefill_mode)
-        model.prefill(ptoks[:64], 0, st)  # warm: buffers, code objects
+        model.prefill(ptoks, 0, st)  # warm: buffers, code objects, hipBLASLt plans
         sync_all(None, torch_mod)
         t0 = time.perf_counter()
         model.prefill(ptoks, 0, st)
@@ -361,10 +361,11 @@ def main():
         flops = 2.0 * args.prefill_tokens * c.n_layers * layer_params  # matrix products only
         prefill = {"tokens": args.prefill_tokens, "ms": round(pf_s * 1e3, 2),
                    "tok_s": round(args.prefill_tokens / pf_s, 1),
-                   "mode": {0: "per-token", 1: "batched (f32-input MFMA; split-f16 MFMA for fp8 weights)",
+                   "mode": {0: "per-token", 1: "batched (hipBLASLt for f16 / e4m3 weights, else MFMA kernels)",
                             2: "batched split-f16 MFMA", 3: "batched f32-input MFMA"}[model.get_option(L.OPT_PREFILL)],
-                   "note": "passes of 64 tokens; f32-input MFMA v_mfma_f32_32x32x2_f32 (f32 activations as the "
-                           "reference, peak 157 TF/s) or v_mfma_f32_32x32x16_f16 on exact f16 hi+lo activation pairs",
+                   "note": "f16 / e4m3 weights: passes of 512 tokens, hipBLASLt GEMMs over f16 hi+lo activation "
+                           "pairs (power-of-two row scale, ~22-bit mantissa); other dtypes: passes of 64 tokens on "
+                           "the hand-written MFMA GEMMs (f32 activations as the reference, or split-f16)",
                    "matmul_tflops": round(flops / pf_s / 1e12, 1)}
         # run_perplexity's loop (xh_perplexity): the same tokens, every token's logits and
         # sample_prob of the next one on the device

@@ -148,8 +148,8 @@ int xh_prefill(xh_ctx* ctx, const int* tokens, int n, int pos0, int want_logits,
 /* Perplexity scoring, the loop of run_perplexity (src/main.cpp:243-254) in one call: forward
  * tokens[0..n-1) at positions pos0.. with logits and write probs_out[i] =
  * Sampler::sample_prob(tokens[i+1]) (src/sampler.cpp:3-17; n-1 floats, caller-owned).  The
- * logits stay on the device; with XH_OPT_PREFILL on, passes of 64 tokens compute every
- * token's logits with one lm_head GEMM.  n >= 2.  The caller takes log and sums, as the
+ * logits stay on the device; with XH_OPT_PREFILL on, each pass computes every token's logits
+ * with one lm_head GEMM.  n >= 2.  The caller takes log and sums, as the
  * reference does in double. */
 int xh_perplexity(xh_ctx* ctx, const int* tokens, int n, int pos0, float* probs_out);
 
@@ -180,13 +180,15 @@ int xh_set_graphs(xh_ctx* ctx, int enable);
 
 /* Launch-structure variants.  XH_OPT_FUSE_ATTN_WO (default 1): 1 = attention and Wo (+ residual)
  * in one launch with an in-launch hand-off (attn_wo.h); 0 = two launches.  Same math. */
-/* XH_OPT_PREFILL (default 1): xh_prefill / xh_perplexity process the prompt in passes of up to
- * 64 tokens, each weight matrix streamed once per pass into MFMA GEMMs (prefill.h): 1 = f32-input
- * MFMA (activations exactly as the reference), except fp8 weights, which take the split-f16
- * MFMA (activations as exact f16 hi + lo pairs under a power-of-two row scale, ≈22-bit
- * mantissa; measured faster there); 2 = split-f16 wherever the weights convert exactly to
- * f16 (f16, fp8); 3 = f32-input MFMA only; 0 = one forward per token (the reference's loop,
- * src/main.cpp:94-100).  Same math per token up to f32 rounding. */
+/* XH_OPT_PREFILL (default 1): xh_prefill / xh_perplexity process the prompt in passes, each
+ * weight matrix streamed once per pass into a GEMM (prefill.h).  1 = f16 and e4m3 weights on
+ * hipBLASLt in passes of 512 tokens, activations as exact f16 hi + lo pairs under a
+ * power-of-two row scale (≈22-bit mantissa, f32 accumulation); e5m2 on the split-f16 MFMA
+ * kernel, other dtypes on the f32-input MFMA kernel (activations exactly as the reference),
+ * passes of 64 tokens when any layer's GEMM is off hipBLASLt; 2 = the split-f16 MFMA kernel
+ * wherever the weights convert exactly to f16 (f16, fp8); 3 = f32-input MFMA only; 0 = one
+ * forward per token (the reference's loop, src/main.cpp:94-100).  Same math per token up to
+ * f32 rounding. */
 /* XH_OPT_PREFILL_GLU_SPLIT (default 1): where the W2 GEMM takes split-f16 input, the GLU
  * epilogue of the W1/W3 GEMM writes those f16 hi/lo fragments directly (one launch); 0 = GLU to
  * f32 first, then split in the W2 GEMM's input pass (two launches).  Bit-identical results; a

@@ -142,8 +142,9 @@ def test_prefill_matches_oracle(name, context, engine):
 @pytest.mark.parametrize("name", FIXTURES)
 @pytest.mark.parametrize("n", [1, 37, 64, 150])
 def test_batched_prefill_matches_oracle(name, n, mode):
-    """xh_prefill's batched path (prefill.h: MFMA GEMMs over passes of <= 64 tokens, causal
-    attention per token) vs the oracle's token-by-token HYDRATE loop: last logits, every
+    """xh_prefill's batched path (prefill.h: hipBLASLt GEMMs over passes of <= 512 tokens for
+    f16 / e4m3 weights, MFMA GEMMs over passes of <= 64 tokens otherwise; causal attention per
+    token) vs the oracle's token-by-token HYDRATE loop: last logits, every
     layer's K and V rows, and the greedy continuation after it.  mode 1: the default choice
     per dtype; 2: split-f16 MFMA wherever the weights allow (f16 / fp8); 3: f32-input MFMA."""
     xf = XalmFile(fixture_path(name + ".xalm"))
@@ -168,6 +169,33 @@ def test_batched_prefill_matches_oracle(name, n, mode):
     for i, t in enumerate(nxt):
         om.forward(t, n + i)
     check(st.logits(), om.logits(), name, "prefill")
+
+
+@pytest.mark.parametrize("name", ["tiny_mistral_f16", "tiny_mistral_f8_e4m3", "small_llama_f16"])
+def test_blas_prefill_multi_pass_matches_oracle(name):
+    """XH_OPT_PREFILL 1 on f16 / e4m3 weights: hipBLASLt passes of 512 tokens; 700 tokens = a
+    full pass and a 188-token one (the second attends over the first pass's K/V rows).  Last
+    logits and every layer's K/V rows vs the oracle's token loop, then the perplexity path over
+    600 tokens (lm_head as one hipBLASLt GEMM per pass, or 64-token slices for bf16 lm_heads)."""
+    xf = XalmFile(fixture_path(name + ".xalm"))
+    gm = Model.from_xalm(xf, context=1024)
+    om = O.OracleModel.from_xalm(xf, context=1024)
+    n = 700
+    toks = [1] + [3 + (i * 37) % 280 for i in range(n - 1)]
+    st = InferenceState(gm.config)
+    gm.prefill(toks, 0, st)
+    for pos, tok in enumerate(toks):
+        om.forward(tok, pos, L.OUTPUT_LOGITS if pos == len(toks) - 1 else L.HYDRATE_KV_CACHE)
+    check(st.logits(), om.logits(), name, "prefill")
+    for layer in range(gm.config.n_layers):
+        for which in (0, 1):
+            a = gm.kv_read(layer, which, 0, n).view(np.float16).astype(np.float32)
+            b = om.kv(layer, which)[:n].view(np.float16).astype(np.float32)
+            assert np.abs(a - b).max() <= 2e-3 * max(1.0, np.abs(b).max()), (layer, which)
+    gm.close()
+    gm2 = Model.from_xalm(xf, context=1024)
+    om2 = O.OracleModel.from_xalm(xf, context=1024)
+    check_probs(gm2.token_probs(toks[:600]), om2, toks[:600], name)
 
 
 def synthetic_pair(wdt, dim=256, hidden=512, n_layers=2, vocab=512, context=256):
@@ -392,7 +420,8 @@ def check_probs(got, om, toks, fixture=None):
 @pytest.mark.parametrize("name", ["tiny_mistral_f16", "tiny_mistral_bf16", "tiny_mistral_f8_e4m3",
                                   "small_llama_f16"])
 def test_perplexity_probs_match_oracle(name, prefill):
-    # xh_perplexity: batched passes (prefill 1: 89 tokens = a full 64-token pass + 25, lm_head
+    # xh_perplexity: batched passes (prefill 2 / 3 and bf16: 89 tokens = a full 64-token pass + 25;
+    # prefill 1 on f16 / e4m3: one hipBLASLt pass; lm_head
     # as one GEMM per pass) and the token loop (prefill 0)
     xf = XalmFile(fixture_path(name + ".xalm"))
     gm = Model.from_xalm(xf, context=256)

@@ -32,10 +32,20 @@ def main():
         m.set_option(getattr(L, "OPT_" + k), int(v))
     st = InferenceState(c)
     prompt = bench.prompt_tokens(c.vocab_size)
-    m.prefill(prompt, 0, st)
-    m.decode_greedy(len(prompt), 50)
+    if w["kv_prefill"]:
+        # configs[3]: a filled 32k ring, decode right after it (kv_len = max_seq_len)
+        for layer in range(c.n_layers):
+            m.kv_fill_synthetic(layer, 0, 0, w["kv_prefill"], 5000 + 2 * layer, 1.0)
+            m.kv_fill_synthetic(layer, 1, 0, w["kv_prefill"], 5001 + 2 * layer, 1.0)
+        pos = w["kv_prefill"]
+        m.prefill(prompt[:1], pos, st)
+        pos += 1
+    else:
+        m.prefill(prompt, 0, st)
+        pos = len(prompt)
+    m.decode_greedy(pos, 20)
     m.debug_trace(16)
-    m.decode_greedy(len(prompt) + 50, 3)
+    m.decode_greedy(pos + 20, 3)
     tr = m.debug_trace(0).astype(np.int64)
     spans = []
     t0 = None

@@ -25,7 +25,9 @@
 
 namespace xalm {
 
-constexpr int PF_TOK = 64;       // tokens per pass (two MFMA token tiles)
+constexpr int PF_TOK = 64;       // tokens per pass of the hand-written MFMA GEMMs (two token tiles)
+constexpr int PF_TOK_BLAS = 512; // tokens per pass of the hipBLASLt GEMMs (xalm_hip.hip pf_blas)
+constexpr int PF_TOK_MAX = PF_TOK_BLAS;
 constexpr int PF_THREADS = 256;  // 4 waves
 constexpr int PF_WAVES = PF_THREADS / 64;
 
@@ -174,6 +176,14 @@ __host__ __device__ inline size_t frag_off(const int tt, const int c, const int 
                                            const int M) {
     return ((((size_t)tt * n_c + c) * M + m) * 64 + lane) * 8;  // in f16 elements
 }
+// offset (f16 elements) of X[t][k .. k+8) in the split layout: E > 0 the fragment layout above,
+// E == 0 plain row-major [t][K] (the hipBLASLt GEMM's B operand)
+__device__ __forceinline__ size_t split_off(const int t, const int k, const int K, const int E) {
+    if (E == 0) return (size_t)t * K + k;
+    const int M = E / 8, n_c = K / (2 * E);
+    const int c = k / (2 * E), r = k - c * 2 * E, hh = r / E, m = (r - hh * E) / 8;
+    return frag_off(t >> 5, c, m, (t & 31) + 32 * hh, n_c, M);
+}
 
 // one workgroup per token row (grid = 32 x token tiles; rows past n are zero): s_t, hi, lo in
 // the fragment layout, inv_s[t] = 1 / s_t
@@ -181,11 +191,9 @@ __global__ __launch_bounds__(256) void prefill_split_kernel(const float* x, int 
                                                             uint16_t* xl, float* inv_s) {
     __shared__ float red[4];
     const int t = blockIdx.x;
-    const int M = E / 8, n_c = K / (2 * E);
     if (t >= n) {
         for (int i = threadIdx.x; i < K / 8; i += 256) {
-            const int k = 8 * i, c = k / (2 * E), r = k - c * 2 * E, hh = r / E, m = (r - hh * E) / 8;
-            const size_t o = frag_off(t >> 5, c, m, (t & 31) + 32 * hh, n_c, M);
+            const size_t o = split_off(t, 8 * i, K, E);
             *(u32x4*)(xh + o) = u32x4{0u, 0u, 0u, 0u};
             *(u32x4*)(xl + o) = u32x4{0u, 0u, 0u, 0u};
         }
@@ -205,7 +213,7 @@ __global__ __launch_bounds__(256) void prefill_split_kernel(const float* x, int 
     if (ok) frexpf(m, &e);  // m = f * 2^e, f in [0.5, 1)
     const float s = ok ? ldexpf(1.f, 15 - e) : 1.f;
     for (int i = threadIdx.x; i < K / 8; i += 256) {
-        const int k = 8 * i, c = k / (2 * E), r = k - c * 2 * E, hh = r / E, mm = (r - hh * E) / 8;
+        const int k = 8 * i;
         const float4 a = *(const float4*)(xr + k), b = *(const float4*)(xr + k + 4);
         const float v[8] = {a.x * s, a.y * s, a.z * s, a.w * s, b.x * s, b.y * s, b.z * s, b.w * s};
         f16x8 hi, lo;
@@ -214,7 +222,7 @@ __global__ __launch_bounds__(256) void prefill_split_kernel(const float* x, int 
             hi[j] = (_Float16)v[j];
             lo[j] = (_Float16)(v[j] - (float)hi[j]);
         }
-        const size_t o = frag_off(t >> 5, c, mm, (t & 31) + 32 * hh, n_c, M);
+        const size_t o = split_off(t, k, K, E);
         *(f16x8*)(xh + o) = hi;
         *(f16x8*)(xl + o) = lo;
     }
@@ -229,11 +237,7 @@ __global__ __launch_bounds__(256) void prefill_rmsnorm_split_kernel(const float*
                                                                     uint16_t* xl, float* inv_s) {
     __shared__ float red[4];
     const int t = blockIdx.x;
-    const int M = E / 8, n_c = dim / (2 * E);
-    auto frag = [&](const int k) {
-        const int c = k / (2 * E), r = k - c * 2 * E, hh = r / E, m = (r - hh * E) / 8;
-        return frag_off(t >> 5, c, m, (t & 31) + 32 * hh, n_c, M);
-    };
+    auto frag = [&](const int k) { return split_off(t, k, dim, E); };
     if (t >= n) {
         for (int i = threadIdx.x; i < dim / 8; i += 256) {
             const size_t o = frag(8 * i);
@@ -287,16 +291,14 @@ __global__ __launch_bounds__(256) void prefill_rmsnorm_split_kernel(const float*
 // straight into the split-f16 fragments of the W2 GEMM's input: one launch instead of GLU
 // epilogue + split.  The row (hidden f32) is held in dynamic LDS between the max and the split
 // (grid = 32 x token tiles; rows past n are zero)
+// part_s (nullable): per-token factor of the partials (the hipBLASLt GEMM's 1 / s of its input)
 __global__ __launch_bounds__(1024) void prefill_glu_split_kernel(const float* part, int ks, int n, int hidden, int act,
-                                                                int E, uint16_t* xh, uint16_t* xl, float* inv_s) {
+                                                                int E, uint16_t* xh, uint16_t* xl, float* inv_s,
+                                                                const float* part_s) {
     extern __shared__ float hrow[];
     __shared__ float red[16];
     const int t = blockIdx.x;
-    const int M = E / 8, n_c = hidden / (2 * E);
-    auto frag = [&](const int k) {
-        const int c = k / (2 * E), r = k - c * 2 * E, hh = r / E, m = (r - hh * E) / 8;
-        return frag_off(t >> 5, c, m, (t & 31) + 32 * hh, n_c, M);
-    };
+    auto frag = [&](const int k) { return split_off(t, k, hidden, E); };
     if (t >= n) {
         for (int i = threadIdx.x; i < hidden / 8; i += 1024) {
             const size_t o = frag(8 * i);
@@ -314,6 +316,10 @@ __global__ __launch_bounds__(1024) void prefill_glu_split_kernel(const float* pa
             const float2 p = *(const float2*)(part + ((size_t)s * n + t) * rows + 2 * i);
             v0 += p.x;
             v1 += p.y;
+        }
+        if (part_s) {
+            v0 *= part_s[t];
+            v1 *= part_s[t];
         }
         const float h = act_fn(act, v0) * v1;
         hrow[i] = h;
@@ -476,6 +482,7 @@ __global__ __launch_bounds__(PF_THREADS) void prefill_gemm16_kernel(const PfGemm
 // Per-pass token scalars
 struct PfEpiArgs {
     const float* part;  // [ks][n][rows]
+    const float* part_s;  // nullable: [n] factor of token t's summed partials (hipBLASLt: 1 / s_t)
     int ks, n, rows;
     int epi;            // EPI_QKV / EPI_RESID / EPI_GLU / EPI_STORE
     float* out;         // RESID: X [n][rows] (+=); GLU: H [n][rows/2]; STORE: [n][out_stride]
@@ -504,6 +511,10 @@ __global__ __launch_bounds__(256) void prefill_epi_kernel(const PfEpiArgs a) {
         const float* p = a.part + ((size_t)s * a.n + t) * a.rows + r;
         v0 += p[0];
         if (two) v1 += p[1];
+    }
+    if (a.part_s) {
+        v0 *= a.part_s[t];
+        v1 *= a.part_s[t];
     }
     if (a.epi == EPI_RESID) {
         float* o = a.out + (size_t)t * a.rows + r;

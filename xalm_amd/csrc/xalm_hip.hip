@@ -16,11 +16,13 @@
 //     gemv<PRO_PLAIN, EPI_RESID>    W2, x += .
 //   gemv<PRO_RMSNORM, EPI_STORE>    final rmsnorm + lm_head -> logits   (OUTPUT_LOGITS)
 //   gemv<PRO_RMSNORM, EPI_LOGITS>   ... + per-workgroup argmax candidates (greedy graph)
-// fuse_level 0 launches attention and Wo separately.  Prompts go through prefill.h (passes of
-// 64 tokens on MFMA) unless XH_OPT_PREFILL is 0.  (Round 2's one-launch engines — persistent,
+// fuse_level 0 launches attention and Wo separately.  Prompts go through prefill.h unless
+// XH_OPT_PREFILL is 0: passes of 512 tokens whose GEMMs run on hipBLASLt (f16 / e4m3 weights,
+// split-f16 activations), else passes of 64 tokens on the hand-written MFMA GEMMs.  (Round 2's one-launch engines — persistent,
 // LDS-DMA stream, qkv+attention+Wo, column-form attention — measured slower and were removed;
 // DESIGN.md §4.5 / §4.9 keep the measurements.)
 #include <hip/hip_runtime.h>
+#include <hipblaslt/hipblaslt.h>
 #include <fcntl.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
@@ -33,6 +35,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <map>
 #include <string>
 #include <thread>
 #include <vector>
@@ -117,25 +120,39 @@ struct xh_ctx {
     unsigned* aw_sync = nullptr;
     // batched prefill (prefill.h), buffers allocated on first use
     bool prefill_batched = true;
-    // XH_OPT_PREFILL: 1 = split-f16 GEMMs for fp8 weights (measured faster), f32 MFMA otherwise;
-    // 2 = split-f16 wherever the weights convert exactly; 3 = f32 MFMA only
+    // XH_OPT_PREFILL: 1 = hipBLASLt for f16 / e4m3 weights, the split-f16 MFMA kernel for e5m2,
+    // f32 MFMA otherwise; 2 = split-f16 MFMA wherever the weights convert exactly; 3 = f32 MFMA only
     int prefill_gemm = 1;
+    int pf_pass = 0;                             // tokens per pass of the current prefill
+    bool pf_scaled = false;                      // the last pf_gemm's partials carry 1 / s_t (pf_xs)
+    // hipBLASLt (created on the first prompt that uses it): handle, workspace, plans per shape
+    hipblasLtHandle_t blas = nullptr;
+    void* blas_ws = nullptr;
+    struct BlasPlan {
+        hipblasLtMatmulDesc_t md = nullptr;
+        hipblasLtMatrixLayout_t la = nullptr, lb = nullptr, lc = nullptr;
+        hipblasLtMatmulAlgo_t algo{};
+        bool ready = false;
+    };
+    std::map<std::vector<int>, BlasPlan> blas_plans;
     bool pf_split_ready = false;                 // pf_norm left the next GEMM's split input
     bool pf_glu_split = true;                    // XH_OPT_PREFILL_GLU_SPLIT: fused GLU -> split input
     bool pf_alloc = false;
-    uint16_t *pf_xh = nullptr, *pf_xl = nullptr; // [PF_TOK][max K] f16 halves of a GEMM input
-    float* pf_xs = nullptr;                      // [PF_TOK] 1 / row scale
-    int* pf_tok = nullptr;                       // [PF_TOK]
-    float *pf_x = nullptr, *pf_xn = nullptr;     // [PF_TOK][dim]
-    float *pf_q = nullptr, *pf_att = nullptr;    // [PF_TOK][q_dim]
-    float* pf_h = nullptr;                       // [PF_TOK][hidden]
-    float* pf_part = nullptr;                    // [PF_PART_ROWS][PF_TOK] split-K partials
-    StepParams* pf_sp = nullptr;                 // [PF_TOK] per-token attention scalars
-    float *pf_po = nullptr, *pf_pml = nullptr;   // [PF_TOK][nsplit][q_dim], [PF_TOK][nsplit][n_heads][2]
-    int* pf_cnt = nullptr;                       // [PF_TOK][n_kv_heads] split tickets
+    // T = PF_TOK_MAX tokens (the largest pass)
+    uint16_t* pf_xh = nullptr;                   // [2T][max K] f16 halves of a GEMM input (pf_alloc)
+    uint16_t* pf_xl = nullptr;                   // [PF_TOK][max K] the split kernel's lo fragments
+    float* pf_xs = nullptr;                      // [T] 1 / row scale
+    int* pf_tok = nullptr;                       // [T]
+    float *pf_x = nullptr, *pf_xn = nullptr;     // [T][dim]
+    float *pf_q = nullptr, *pf_att = nullptr;    // [T][q_dim]
+    float* pf_h = nullptr;                       // [T][hidden]
+    float* pf_part = nullptr;                    // split-K partials [ks][n][rows] (pf_part_floats)
+    StepParams* pf_sp = nullptr;                 // [T] per-token attention scalars
+    float *pf_po = nullptr, *pf_pml = nullptr;   // [T][nsplit][q_dim], [T][nsplit][n_heads][2]
+    int* pf_cnt = nullptr;                       // [T][n_kv_heads] split tickets
     // xh_perplexity: per-token logits of a pass, targets, probabilities (allocated on first use)
-    float* pf_logits = nullptr;                  // [PF_TOK][vocab]
-    int* pf_tgt = nullptr;                       // [PF_TOK]
+    float* pf_logits = nullptr;                  // [T][vocab]
+    int* pf_tgt = nullptr;                       // [T]
     int* ppl_tgt = nullptr;                      // [ppl_cap] targets (per-token path)
     float* ppl_prob = nullptr;                   // [ppl_cap]
     int ppl_cap = 0;
@@ -618,25 +635,94 @@ constexpr int PF_RT = 2;                // 32-row tiles per GEMM wave (1: -11 %,
 constexpr int PF_RT16 = 4;              // 32-row tiles per split-f16 GEMM wave
 constexpr size_t PF_PART_ROWS = 32 * PF_RT16 * PF_WAVE_TARGET;  // >= ks * rows (ks * ceil(rows/(32 RT)) <= target)
 
+constexpr int PF_CLS_CHUNK = (int)(PF_PART_ROWS / 4);  // lm_head rows per GEMM (ks <= 4 fits the partials)
+constexpr size_t PF_BLAS_WS = 256ull << 20;            // hipBLASLt workspace
+
+// partials buffer: the MFMA kernels' K slices of 64 tokens, or the hipBLASLt GEMM's two halves
+// (hi, lo) of a 512-token pass over the widest matrix
+size_t pf_part_floats(const xh_ctx* ctx) {
+    const xh_config& c = ctx->c;
+    const int rows = std::max({ctx->q_dim + 2 * ctx->kv_dim, 2 * c.hidden_dim, c.dim, std::min(c.vocab_size, PF_CLS_CHUNK)});
+    return std::max(PF_PART_ROWS * PF_TOK, (size_t)2 * PF_TOK_MAX * rows);
+}
+
 int pf_alloc(xh_ctx* ctx) {
     if (ctx->pf_alloc) return 0;
     const xh_config& c = ctx->c;
+    const size_t T = PF_TOK_MAX;
     int rc;
-    if ((rc = dmalloc(ctx, &ctx->pf_tok, (size_t)PF_TOK)) || (rc = dmalloc(ctx, &ctx->pf_x, (size_t)PF_TOK * c.dim)) ||
-        (rc = dmalloc(ctx, &ctx->pf_xn, (size_t)PF_TOK * c.dim)) ||
-        (rc = dmalloc(ctx, &ctx->pf_q, (size_t)PF_TOK * ctx->q_dim)) ||
-        (rc = dmalloc(ctx, &ctx->pf_att, (size_t)PF_TOK * ctx->q_dim)) ||
-        (rc = dmalloc(ctx, &ctx->pf_h, (size_t)PF_TOK * c.hidden_dim)) ||
-        (rc = dmalloc(ctx, &ctx->pf_part, PF_PART_ROWS * PF_TOK)) || (rc = dmalloc(ctx, &ctx->pf_sp, (size_t)PF_TOK)) ||
-        (rc = dmalloc(ctx, &ctx->pf_po, (size_t)PF_TOK * ctx->nsplit * ctx->q_dim)) ||
-        (rc = dmalloc(ctx, &ctx->pf_pml, (size_t)PF_TOK * ctx->nsplit * c.n_heads * 2)) ||
-        (rc = dmalloc(ctx, &ctx->pf_cnt, (size_t)PF_TOK * c.n_kv_heads)))
+    if ((rc = dmalloc(ctx, &ctx->pf_tok, T)) || (rc = dmalloc(ctx, &ctx->pf_x, T * c.dim)) ||
+        (rc = dmalloc(ctx, &ctx->pf_xn, T * c.dim)) || (rc = dmalloc(ctx, &ctx->pf_q, T * ctx->q_dim)) ||
+        (rc = dmalloc(ctx, &ctx->pf_att, T * ctx->q_dim)) || (rc = dmalloc(ctx, &ctx->pf_h, T * c.hidden_dim)) ||
+        (rc = dmalloc(ctx, &ctx->pf_part, pf_part_floats(ctx))) || (rc = dmalloc(ctx, &ctx->pf_sp, T)) ||
+        (rc = dmalloc(ctx, &ctx->pf_po, T * ctx->nsplit * ctx->q_dim)) ||
+        (rc = dmalloc(ctx, &ctx->pf_pml, T * ctx->nsplit * c.n_heads * 2)) ||
+        (rc = dmalloc(ctx, &ctx->pf_cnt, T * c.n_kv_heads)))
         return rc;
+    // pf_xh: the split-kernel fragments of <= 64 tokens, or hi rows then lo rows of a
+    // hipBLASLt pass (one B operand of 2n columns); pf_xl: the split kernel's lo fragments
     const size_t kmax = std::max({(size_t)c.dim, (size_t)c.hidden_dim, (size_t)ctx->q_dim});
-    if ((rc = dmalloc(ctx, &ctx->pf_xh, PF_TOK * kmax)) || (rc = dmalloc(ctx, &ctx->pf_xl, PF_TOK * kmax)) ||
-        (rc = dmalloc(ctx, &ctx->pf_xs, (size_t)PF_TOK)))
+    if ((rc = dmalloc(ctx, &ctx->pf_xh, 2 * T * kmax)) || (rc = dmalloc(ctx, &ctx->pf_xl, PF_TOK * kmax)) ||
+        (rc = dmalloc(ctx, &ctx->pf_xs, T)))
         return rc;
     ctx->pf_alloc = true;
+    return 0;
+}
+
+#define BLAS_TRY(ctx, expr)                                                                          \
+    do {                                                                                             \
+        hipblasStatus_t _s = (expr);                                                                 \
+        if (_s != HIPBLAS_STATUS_SUCCESS)                                                            \
+            return set_err((ctx), XH_E_HIP, "%s failed: hipBLASLt status %d", #expr, (int)_s);       \
+    } while (0)
+
+// Y[n][rows] (f32) = X[n][K] (f16) . W[rows][K]^T on hipBLASLt.  Column-major view: D (rows x n,
+// ld rows) = op(A) B with A = W stored K x rows (ld K, transposed), B = X stored K x n (ld K).
+// f16 weights: f32 compute; e4m3 weights: f32 accumulation over f16 products (FAST_16F; e4m3 is
+// exact in f16).  One plan per (dtype, rows, K, n), algorithm = the heuristic's first.
+int blas_gemm(xh_ctx* ctx, int dt, const void* w, int K, int rows, const uint16_t* x, int n, float* y) {
+    if (!ctx->blas) {
+        BLAS_TRY(ctx, hipblasLtCreate(&ctx->blas));
+        char* ws = nullptr;
+        int rc = dmalloc(ctx, &ws, PF_BLAS_WS);
+        if (rc) return rc;
+        ctx->blas_ws = ws;
+    }
+    const std::vector<int> key{dt, rows, K, n};
+    auto it = ctx->blas_plans.find(key);
+    if (it == ctx->blas_plans.end()) {
+        xh_ctx::BlasPlan& p = ctx->blas_plans[key];  // destroyed with the context, even half-built
+        const bool f8 = dt == XH_F8_E4M3;
+        BLAS_TRY(ctx, hipblasLtMatmulDescCreate(&p.md, f8 ? HIPBLAS_COMPUTE_32F_FAST_16F : HIPBLAS_COMPUTE_32F,
+                                                HIP_R_32F));
+        const hipblasOperation_t opT = HIPBLAS_OP_T, opN = HIPBLAS_OP_N;
+        BLAS_TRY(ctx, hipblasLtMatmulDescSetAttribute(p.md, HIPBLASLT_MATMUL_DESC_TRANSA, &opT, sizeof opT));
+        BLAS_TRY(ctx, hipblasLtMatmulDescSetAttribute(p.md, HIPBLASLT_MATMUL_DESC_TRANSB, &opN, sizeof opN));
+        BLAS_TRY(ctx, hipblasLtMatrixLayoutCreate(&p.la, f8 ? HIP_R_8F_E4M3 : HIP_R_16F, K, rows, K));
+        BLAS_TRY(ctx, hipblasLtMatrixLayoutCreate(&p.lb, HIP_R_16F, K, n, K));
+        BLAS_TRY(ctx, hipblasLtMatrixLayoutCreate(&p.lc, HIP_R_32F, rows, n, rows));
+        hipblasLtMatmulPreference_t pref;
+        BLAS_TRY(ctx, hipblasLtMatmulPreferenceCreate(&pref));
+        size_t wss = PF_BLAS_WS;
+        hipblasLtMatmulHeuristicResult_t heur[1];
+        int nret = 0;
+        hipblasStatus_t st = hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES,
+                                                                   &wss, sizeof wss);
+        if (st == HIPBLAS_STATUS_SUCCESS)
+            st = hipblasLtMatmulAlgoGetHeuristic(ctx->blas, p.md, p.la, p.lb, p.lc, p.lc, pref, 1, heur, &nret);
+        hipblasLtMatmulPreferenceDestroy(pref);
+        if (st != HIPBLAS_STATUS_SUCCESS || nret < 1)
+            return set_err(ctx, XH_E_HIP, "hipBLASLt: no algorithm for %d x %d x %d (dtype %d), status %d", rows, K, n,
+                           dt, (int)st);
+        p.algo = heur[0].algo;
+        p.ready = true;
+        it = ctx->blas_plans.find(key);
+    }
+    const xh_ctx::BlasPlan& p = it->second;
+    if (!p.ready) return set_err(ctx, XH_E_HIP, "hipBLASLt: plan %d x %d x %d failed earlier", rows, K, n);
+    const float alpha = 1.f, beta = 0.f;
+    BLAS_TRY(ctx, hipblasLtMatmul(ctx->blas, p.md, &alpha, w, p.la, x, p.lb, &beta, y, p.lc, y, p.lc, &p.algo,
+                                  ctx->blas_ws, PF_BLAS_WS, ctx->stream));
     return 0;
 }
 
@@ -676,62 +762,93 @@ void pf_gemm16_t(const PfGemm16Args& a, hipStream_t s) {
     hipLaunchKernelGGL((prefill_gemm16_kernel<DT, PF_RT16>), dim3((waves + PF_WAVES - 1) / PF_WAVES), dim3(PF_THREADS),
                        0, s, a);
 }
-// E of the split-f16 path when the GEMM over W (dtype dt, [rows][K]) takes it, else 0
-// (XH_OPT_PREFILL 1: fp8 weights; 2: f16 and fp8; 3: never; a K slicing must exist)
-int pf_split_E(const xh_ctx* ctx, int dt, int K, int rows) {
+// XH_OPT_PREFILL 1: hipBLASLt runs the GEMM over weights of dtype dt (f16, or e4m3 whose codes
+// all convert exactly in hardware: kdt keeps the _EXACT dtypes off this path)
+bool pf_blas(const xh_ctx* ctx, int dt) { return ctx->prefill_gemm == 1 && (dt == XH_F16 || dt == XH_F8_E4M3); }
+// Layout of the split-f16 input of the GEMM over W (dtype dt, [rows][K]): 0 = row-major (the
+// hipBLASLt path), E > 0 = the split-f16 kernel's fragments, -1 = no split (f32-input MFMA).
+// XH_OPT_PREFILL 1: hipBLASLt for f16 / e4m3, the split kernel for e5m2; 2: the split kernel
+// for f16 and fp8; 3: never split.  The split kernel also needs a K slicing.
+int pf_layout(const xh_ctx* ctx, int dt, int K, int rows) {
+    if (pf_blas(ctx, dt)) return 0;
     const bool f8 = dt == XH_F8_E4M3 || dt == XH_F8_E5M2;
-    if (!(ctx->prefill_gemm == 2 || (ctx->prefill_gemm == 1 && f8))) return 0;
-    if (dt != XH_F16 && !f8) return 0;
+    if (!(ctx->prefill_gemm == 2 || (ctx->prefill_gemm == 1 && f8))) return -1;
+    if (dt != XH_F16 && !f8) return -1;
     const int E = elems_per_16b(dt);
-    return pf_ks16(rows, K, E) ? E : 0;
+    return pf_ks16(rows, K, E) ? E : -1;
+}
+// split-f16 halves of a pass's rows: hi into pf_xh; lo into pf_xl (fragments) or right after
+// the hi rows (row-major: one B operand of 2n columns)
+uint16_t* pf_lo(xh_ctx* ctx, int layout, int n, int K) {
+    return layout ? ctx->pf_xl : ctx->pf_xh + (size_t)n * K;
+}
+// grid of the split kernels: one workgroup per token row, fragments padded to 32-token tiles
+int pf_split_grid(int layout, int n) { return layout ? 32 * ((n + 31) / 32) : n; }
+// Tokens per pass: 512 when every GEMM of the pass runs on hipBLASLt (the lm_head of a
+// perplexity pass aside: it runs on 64-token slices when it cannot), else 64 (the MFMA kernels'
+// two token tiles)
+int pf_pass_tokens(const xh_ctx* ctx) {
+    for (const LayerW& w : ctx->L)
+        if (!pf_blas(ctx, kdt(w.qkv_dt, w.qkv_x)) || !pf_blas(ctx, kdt(w.wo_dt, w.wo_x)) ||
+            !pf_blas(ctx, kdt(w.w13_dt, w.w13_x)) || !pf_blas(ctx, kdt(w.w2_dt, w.w2_x)))
+            return PF_TOK;
+    return PF_TOK_BLAS;
 }
 // rmsnorm of the pass's rows (pf_x) as the input of the GEMM over W (dt, [rows][dim]): written
-// straight into the split-f16 fragments when that GEMM takes the split path (one launch)
+// straight into the split-f16 halves when that GEMM takes a split input (one launch)
 void pf_norm(xh_ctx* ctx, const void* nw, int ndt, int m, int dt, int rows) {
     const xh_config& c = ctx->c;
-    const int E = pf_split_E(ctx, dt, c.dim, rows);
-    if (E) {
-        hipLaunchKernelGGL(prefill_rmsnorm_split_kernel, dim3(32 * ((m + 31) / 32)), dim3(256), 0, ctx->stream,
-                           (const float*)ctx->pf_x, c.dim, nw, ndt, c.norm_eps, m, E, ctx->pf_xh, ctx->pf_xl, ctx->pf_xs);
+    const int lay = pf_layout(ctx, dt, c.dim, rows);
+    if (lay >= 0) {
+        hipLaunchKernelGGL(prefill_rmsnorm_split_kernel, dim3(pf_split_grid(lay, m)), dim3(256), 0, ctx->stream,
+                           (const float*)ctx->pf_x, c.dim, nw, ndt, c.norm_eps, m, lay, ctx->pf_xh,
+                           pf_lo(ctx, lay, m, c.dim), ctx->pf_xs);
         ctx->pf_split_ready = true;
     } else {
         hipLaunchKernelGGL(prefill_rmsnorm_kernel, dim3(m), dim3(256), 0, ctx->stream, (const float*)ctx->pf_x, c.dim,
                            nw, ndt, c.norm_eps, ctx->pf_xn);
     }
 }
-// the split-f16 form of pf_gemm for weights exact in f16; 0 = not taken
-int pf_gemm16(xh_ctx* ctx, int dt, const void* w, int K, int rows, const float* x, int n) {
-    const int E = pf_split_E(ctx, dt, K, rows);
-    if (!E) return 0;
-    const int ks = pf_ks16(rows, K, E);
-    if (ctx->pf_split_ready)
-        ctx->pf_split_ready = false;  // pf_norm wrote the fragments of x
-    else
-        hipLaunchKernelGGL(prefill_split_kernel, dim3(32 * ((n + 31) / 32)), dim3(256), 0, ctx->stream, x, K, n, E,
-                           ctx->pf_xh, ctx->pf_xl, ctx->pf_xs);
-    PfGemm16Args a{};
-    a.w = w; a.row_bytes = (size_t)K * (16 / E); a.K = K; a.rows = rows;
-    a.xh = ctx->pf_xh; a.xl = ctx->pf_xl; a.inv_s = ctx->pf_xs; a.n = n; a.ks = ks; a.part = ctx->pf_part;
-    switch (dt) {
-        case XH_F16: pf_gemm16_t<XH_F16>(a, ctx->stream); break;
-        case XH_F8_E4M3: pf_gemm16_t<XH_F8_E4M3>(a, ctx->stream); break;
-        default: pf_gemm16_t<XH_F8_E5M2>(a, ctx->stream); break;
+// Y partials of W[rows][K] . X[n][K] into pf_part ([ks][n][rows]).  Split-f16 paths convert x
+// first unless pf_norm / the fused GLU already left its halves.  0 or an error code.
+int pf_gemm(xh_ctx* ctx, const char* what, int dt, const void* w, int K, int rows, const float* x, int n, int& ks) {
+    const int lay = pf_layout(ctx, dt, K, rows);
+    ctx->pf_scaled = false;
+    if (lay >= 0) {
+        if (ctx->pf_split_ready)
+            ctx->pf_split_ready = false;
+        else
+            hipLaunchKernelGGL(prefill_split_kernel, dim3(pf_split_grid(lay, n)), dim3(256), 0, ctx->stream, x, K, n,
+                               lay, ctx->pf_xh, pf_lo(ctx, lay, n, K), ctx->pf_xs);
     }
-    return ks;
-}
-// Y partials of W[rows][K] . X[n][K]; returns ks (0: dtype / shape not supported)
-int pf_gemm(xh_ctx* ctx, int dt, const void* w, int K, int rows, const float* x, int n) {
-    {
-        const int ks = pf_gemm16(ctx, dt, w, K, rows, x, n);
-        if (ks) return ks;
+    if (lay == 0) {
+        // hi and lo rows as one B operand: partials [2][n][rows], the epilogue scales by 1 / s_t
+        int rc = blas_gemm(ctx, dt, w, K, rows, ctx->pf_xh, 2 * n, ctx->pf_part);
+        if (rc) return rc;
+        ctx->pf_scaled = true;
+        ks = 2;
+        return 0;
+    }
+    if (lay > 0) {
+        PfGemm16Args a{};
+        a.w = w; a.row_bytes = (size_t)K * (16 / lay); a.K = K; a.rows = rows;
+        a.xh = ctx->pf_xh; a.xl = ctx->pf_xl; a.inv_s = ctx->pf_xs; a.n = n; a.ks = pf_ks16(rows, K, lay);
+        a.part = ctx->pf_part;
+        switch (dt) {
+            case XH_F16: pf_gemm16_t<XH_F16>(a, ctx->stream); break;
+            case XH_F8_E4M3: pf_gemm16_t<XH_F8_E4M3>(a, ctx->stream); break;
+            default: pf_gemm16_t<XH_F8_E5M2>(a, ctx->stream); break;
+        }
+        ks = a.ks;
+        return 0;
     }
     const int E = (dt == XH_F8_E4M3_EXACT || dt == XH_F8_E5M2_EXACT) ? 16 : elems_per_16b(dt);
-    if (K % (2 * E)) return 0;
+    if (K % (2 * E) || n > PF_TOK) return set_err(ctx, XH_E_INVALID, "prefill: %s shape not supported", what);
     PfGemmArgs a{};
     a.w = w; a.K = K; a.rows = rows; a.x = x; a.n = n; a.part = ctx->pf_part;
     a.row_bytes = (size_t)K * (16 / E);
     a.ks = pf_ks(rows, K, E);
-    if ((size_t)a.ks * rows > PF_PART_ROWS) return 0;
+    if ((size_t)a.ks * rows > PF_PART_ROWS) return set_err(ctx, XH_E_INVALID, "prefill: %s shape not supported", what);
     hipStream_t s = ctx->stream;
     switch (dt) {
         case XH_F32: pf_gemm_t<XH_F32>(a, s); break;
@@ -742,12 +859,14 @@ int pf_gemm(xh_ctx* ctx, int dt, const void* w, int K, int rows, const float* x,
         case XH_Q8: pf_gemm_t<XH_Q8>(a, s); break;
         case XH_F8_E4M3_EXACT: pf_gemm_t<XH_F8_E4M3_EXACT>(a, s); break;
         case XH_F8_E5M2_EXACT: pf_gemm_t<XH_F8_E5M2_EXACT>(a, s); break;
-        default: return 0;
+        default: return set_err(ctx, XH_E_INVALID, "prefill: %s dtype %d not supported", what, dt);
     }
-    return a.ks;
+    ks = a.ks;
+    return 0;
 }
 void pf_epi(xh_ctx* ctx, PfEpiArgs e) {
     e.part = ctx->pf_part;
+    e.part_s = ctx->pf_scaled ? ctx->pf_xs : nullptr;
     const int threads = e.n * ((e.rows + 1) / 2);
     hipLaunchKernelGGL(prefill_epi_kernel, dim3((threads + 255) / 256), dim3(256), 0, ctx->stream, e);
 }
@@ -789,8 +908,6 @@ bool pf_supported(const xh_ctx* ctx, int n, int pos0) {
     return c.dim % 32 == 0 && c.hidden_dim % 32 == 0 && ctx->q_dim % 32 == 0;
 }
 
-constexpr int PF_CLS_CHUNK = (int)(PF_PART_ROWS / 4);  // lm_head rows per GEMM (ks <= 4 fits the partials)
-
 // tokens[0..n) at positions pos0..: HYDRATE for every token, then the last token's logits.
 // probs (device, n floats) != nullptr: also every token's logits (final rmsnorm + lm_head as
 // one GEMM per pass) and probs[i] = sample_prob(targets[i]) (targets: host, n ints).
@@ -801,11 +918,13 @@ int prefill_batched(xh_ctx* ctx, const int* tokens, int n, int pos0, int want_lo
     if (rc) return rc;
     ctx->pf_split_ready = false;
     if (probs && !ctx->pf_logits &&
-        ((rc = dmalloc(ctx, &ctx->pf_logits, (size_t)PF_TOK * c.vocab_size)) || (rc = dmalloc(ctx, &ctx->pf_tgt, (size_t)PF_TOK))))
+        ((rc = dmalloc(ctx, &ctx->pf_logits, (size_t)PF_TOK_MAX * c.vocab_size)) ||
+         (rc = dmalloc(ctx, &ctx->pf_tgt, (size_t)PF_TOK_MAX))))
         return rc;
-    std::vector<StepParams> sps(PF_TOK);
-    for (int off = 0; off < n; off += PF_TOK) {
-        const int m = std::min(n - off, PF_TOK);
+    const int pass = ctx->pf_pass = pf_pass_tokens(ctx);
+    std::vector<StepParams> sps(pass);
+    for (int off = 0; off < n; off += pass) {
+        const int m = std::min(n - off, pass);
         const int p0 = pos0 + off;
         HIP_TRY(ctx, hipMemcpyAsync(ctx->pf_tok, tokens + off, (size_t)m * sizeof(int), hipMemcpyHostToDevice, ctx->stream));
         for (int t = 0; t < m; t++) {
@@ -826,9 +945,9 @@ int prefill_batched(xh_ctx* ctx, const int* tokens, int n, int pos0, int want_lo
             const LayerW& w = ctx->L[l];
             // attention block (src/infer.cpp:380-452)
             const int qkv_rows = ctx->q_dim + 2 * ctx->kv_dim;
+            int ks = 0;
             pf_norm(ctx, w.attn_norm, w.an_dt, m, kdt(w.qkv_dt, w.qkv_x), qkv_rows);
-            int ks = pf_gemm(ctx, kdt(w.qkv_dt, w.qkv_x), w.wqkv, c.dim, qkv_rows, ctx->pf_xn, m);
-            if (!ks) return set_err(ctx, XH_E_INVALID, "prefill: qkv shape not supported");
+            if ((rc = pf_gemm(ctx, "qkv", kdt(w.qkv_dt, w.qkv_x), w.wqkv, c.dim, qkv_rows, ctx->pf_xn, m, ks))) return rc;
             PfEpiArgs e{};
             e.ks = ks; e.n = m; e.rows = qkv_rows; e.epi = EPI_QKV; e.q = ctx->pf_q;
             e.kcache = ctx->kcache(l); e.vcache = ctx->vcache(l); e.q_dim = ctx->q_dim; e.kv_dim = ctx->kv_dim;
@@ -840,26 +959,28 @@ int prefill_batched(xh_ctx* ctx, const int* tokens, int n, int pos0, int want_lo
             aa.counters = ctx->pf_cnt;
             aa.nsplit = std::min(ctx->nsplit, std::max(1, (p0 + m + ATTN_MIN_T - 1) / ATTN_MIN_T));
             if (!pf_attn(ctx, aa, m)) return set_err(ctx, XH_E_INVALID, "prefill: head shape not instantiated");
-            ks = pf_gemm(ctx, kdt(w.wo_dt, w.wo_x), w.wo, ctx->q_dim, c.dim, ctx->pf_att, m);
-            if (!ks) return set_err(ctx, XH_E_INVALID, "prefill: wo shape not supported");
+            if ((rc = pf_gemm(ctx, "wo", kdt(w.wo_dt, w.wo_x), w.wo, ctx->q_dim, c.dim, ctx->pf_att, m, ks))) return rc;
             e = PfEpiArgs{};
             e.ks = ks; e.n = m; e.rows = c.dim; e.epi = EPI_RESID; e.out = ctx->pf_x;
             pf_epi(ctx, e);
             // feed-forward block (src/infer.cpp:455-494)
             pf_norm(ctx, w.ffn_norm, w.fn_dt, m, kdt(w.w13_dt, w.w13_x), 2 * c.hidden_dim);
-            ks = pf_gemm(ctx, kdt(w.w13_dt, w.w13_x), w.w13, c.dim, 2 * c.hidden_dim, ctx->pf_xn, m);
-            if (!ks) return set_err(ctx, XH_E_INVALID, "prefill: w1/w3 shape not supported");
-            const int E2 = pf_split_E(ctx, kdt(w.w2_dt, w.w2_x), c.hidden_dim, c.dim);
+            if ((rc = pf_gemm(ctx, "w1/w3", kdt(w.w13_dt, w.w13_x), w.w13, c.dim, 2 * c.hidden_dim, ctx->pf_xn, m, ks)))
+                return rc;
+            const int lay2 = pf_layout(ctx, kdt(w.w2_dt, w.w2_x), c.hidden_dim, c.dim);
             // dynamic LDS = one f32 row of h; the kernel adds a static 16-float reduction array
             const size_t glu_lds = (size_t)c.hidden_dim * sizeof(float);
             bool glu_fused = false;
-            if (E2 && ctx->pf_glu_split && glu_lds + 16 * sizeof(float) <= 64 * 1024) {
-                // GLU epilogue straight into the W2 GEMM's split-f16 fragments (one launch); the
-                // size check above is the launch's only precondition, so any error here is real
+            if (lay2 >= 0 && ctx->pf_glu_split && glu_lds + 16 * sizeof(float) <= 64 * 1024) {
+                // GLU epilogue straight into the W2 GEMM's split-f16 input (one launch); the size
+                // check above is the launch's only precondition, so any error here is real.
+                // part_s and inv_s are both pf_xs: a workgroup reads its token's factor before
+                // the barrier and writes the new one after it.
                 HIP_TRY(ctx, hipGetLastError());  // an earlier launch's error is reported as such
-                hipLaunchKernelGGL(prefill_glu_split_kernel, dim3(32 * ((m + 31) / 32)), dim3(1024),
-                                   glu_lds, ctx->stream, (const float*)ctx->pf_part, ks,
-                                   m, c.hidden_dim, c.act, E2, ctx->pf_xh, ctx->pf_xl, ctx->pf_xs);
+                hipLaunchKernelGGL(prefill_glu_split_kernel, dim3(pf_split_grid(lay2, m)), dim3(1024), glu_lds,
+                                   ctx->stream, (const float*)ctx->pf_part, ks, m, c.hidden_dim, c.act, lay2,
+                                   ctx->pf_xh, pf_lo(ctx, lay2, m, c.hidden_dim), ctx->pf_xs,
+                                   (const float*)(ctx->pf_scaled ? ctx->pf_xs : nullptr));
                 HIP_TRY(ctx, hipGetLastError());
                 glu_fused = true;
                 ctx->pf_split_ready = true;
@@ -869,8 +990,7 @@ int prefill_batched(xh_ctx* ctx, const int* tokens, int n, int pos0, int want_lo
                 e.ks = ks; e.n = m; e.rows = 2 * c.hidden_dim; e.epi = EPI_GLU; e.out = ctx->pf_h; e.act = c.act;
                 pf_epi(ctx, e);
             }
-            ks = pf_gemm(ctx, kdt(w.w2_dt, w.w2_x), w.w2, c.hidden_dim, c.dim, ctx->pf_h, m);
-            if (!ks) return set_err(ctx, XH_E_INVALID, "prefill: w2 shape not supported");
+            if ((rc = pf_gemm(ctx, "w2", kdt(w.w2_dt, w.w2_x), w.w2, c.hidden_dim, c.dim, ctx->pf_h, m, ks))) return rc;
             e = PfEpiArgs{};
             e.ks = ks; e.n = m; e.rows = c.dim; e.epi = EPI_RESID; e.out = ctx->pf_x;
             pf_epi(ctx, e);
@@ -883,15 +1003,23 @@ int prefill_batched(xh_ctx* ctx, const int* tokens, int n, int pos0, int want_lo
             hipLaunchKernelGGL(prefill_rmsnorm_kernel, dim3(m), dim3(256), 0, ctx->stream, (const float*)ctx->pf_x, c.dim,
                                (const void*)ctx->final_norm, ctx->final_norm_dt, c.norm_eps, ctx->pf_xn);
             const size_t cls_rb = dev_row_bytes(ctx->wcls_dt, c.dim);
+            const int cls_dt = kdt(ctx->wcls_dt, ctx->wcls_x);
+            // lm_head weights off the hipBLASLt path (bf16 on the fp8 checkpoints): 64-token slices
+            const int tstep = pf_blas(ctx, cls_dt) ? m : PF_TOK;
             for (int r0 = 0; r0 < c.vocab_size; r0 += PF_CLS_CHUNK) {
                 const int rows = std::min(PF_CLS_CHUNK, c.vocab_size - r0);
-                const int ks = pf_gemm(ctx, kdt(ctx->wcls_dt, ctx->wcls_x), (const char*)ctx->wcls + (size_t)r0 * cls_rb,
-                                       c.dim, rows, ctx->pf_xn, m);
-                if (!ks) return set_err(ctx, XH_E_INVALID, "perplexity: lm_head shape not supported");
-                PfEpiArgs e{};
-                e.ks = ks; e.n = m; e.rows = rows; e.epi = EPI_STORE; e.out = ctx->pf_logits + r0;
-                e.out_stride = (size_t)c.vocab_size;
-                pf_epi(ctx, e);
+                for (int t0 = 0; t0 < m; t0 += tstep) {
+                    const int mt = std::min(tstep, m - t0);
+                    int ks = 0;
+                    if ((rc = pf_gemm(ctx, "lm_head", cls_dt, (const char*)ctx->wcls + (size_t)r0 * cls_rb, c.dim, rows,
+                                      ctx->pf_xn + (size_t)t0 * c.dim, mt, ks)))
+                        return rc;
+                    PfEpiArgs e{};
+                    e.ks = ks; e.n = mt; e.rows = rows; e.epi = EPI_STORE;
+                    e.out = ctx->pf_logits + (size_t)t0 * c.vocab_size + r0;
+                    e.out_stride = (size_t)c.vocab_size;
+                    pf_epi(ctx, e);
+                }
             }
             hipLaunchKernelGGL(token_prob_kernel, dim3(m), dim3(1024), 0, ctx->stream, (const float*)ctx->pf_logits,
                                c.vocab_size, (size_t)c.vocab_size, (const int*)ctx->pf_tgt, probs + off);
@@ -1055,6 +1183,14 @@ void xh_destroy(xh_ctx* ctx) {
     hipFree(ctx->pf_logits); hipFree(ctx->pf_tgt); hipFree(ctx->ppl_tgt); hipFree(ctx->ppl_prob);
     hipFree(ctx->pf_part); hipFree(ctx->pf_sp); hipFree(ctx->pf_po); hipFree(ctx->pf_pml); hipFree(ctx->pf_cnt); hipFree(ctx->rope_freq);
     hipFree(ctx->aw_trace);
+    for (auto& kv : ctx->blas_plans) {
+        const xh_ctx::BlasPlan& p = kv.second;
+        for (hipblasLtMatrixLayout_t l : {p.la, p.lb, p.lc})
+            if (l) hipblasLtMatrixLayoutDestroy(l);
+        if (p.md) hipblasLtMatmulDescDestroy(p.md);
+    }
+    if (ctx->blas) hipblasLtDestroy(ctx->blas);
+    hipFree(ctx->blas_ws);
     hipFree(ctx->sink_cos); hipFree(ctx->sink_sin); hipFree(ctx->sp); hipFree(ctx->dec_tokens);
     if (ctx->sp_host) hipHostFree(ctx->sp_host);
     if (ctx->stream) hipStreamDestroy(ctx->stream);
