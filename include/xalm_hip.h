@@ -193,7 +193,10 @@ int xh_set_graphs(xh_ctx* ctx, int enable);
  * epilogue of the W1/W3 GEMM writes those f16 hi/lo fragments directly (one launch); 0 = GLU to
  * f32 first, then split in the W2 GEMM's input pass (two launches).  Bit-identical results; a
  * debug knob so tests cover both routes. */
-enum xh_option { XH_OPT_FUSE_ATTN_WO = 1, XH_OPT_PREFILL = 2, XH_OPT_PREFILL_GLU_SPLIT = 3 };
+/* XH_OPT_PREFILL_ATTN (default 1): the batched path's causal attention on MFMA tiles (32 query
+ * rows x 32-slot K/V tiles per wave, running max/sum, q and p as exact f16 hi + lo pairs);
+ * 0 = one workgroup per token and KV head, split-KV f32 FMA (the decode attention's blocks). */
+enum xh_option { XH_OPT_FUSE_ATTN_WO = 1, XH_OPT_PREFILL = 2, XH_OPT_PREFILL_GLU_SPLIT = 3, XH_OPT_PREFILL_ATTN = 4 };
 int xh_set_option(xh_ctx* ctx, int option, int value);
 int xh_get_option(const xh_ctx* ctx, int option, int* value);
 

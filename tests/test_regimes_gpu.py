@@ -393,3 +393,32 @@ def test_full_size_mistral_within_reference_order_sensitivity():
     assert e_pre <= sens, (e_pre, sens)
     assert e_loop <= sens, (e_loop, sens)
     assert np.argmax(lg_loop) == O.sample_argmax(ref[0]) or np.sort(ref[0])[-1] - np.sort(ref[0])[-2] < 2 * sens
+
+
+@pytest.mark.parametrize("attn", [1, 0])
+@pytest.mark.parametrize("heads,kv_heads,head_dim,wdt", [(8, 2, 128, L.F16), (16, 2, 128, L.F16),
+                                                          (8, 2, 64, L.F8_E4M3), (4, 2, 16, L.BF16)])
+def test_prompt_attention_in_two_prompts(heads, kv_heads, head_dim, wdt, attn):
+    """xh_prefill's causal attention (XH_OPT_PREFILL_ATTN 1: MFMA tiles; 0: per-token split
+    kernel) at every instantiated head shape (QPK 4 / 8 / 2, head_dim 128 / 64 / 16), a prompt
+    of 600 tokens followed by a second prompt of 300 at pos 600 (its rows attend over the first
+    prompt's K/V), against the oracle's token loop: last logits and every K/V row.  f16
+    weights run 512-token passes (attention over a pass boundary), bf16 64-token ones."""
+    c = make_cfg(256, 512, 2, heads, kv_heads, head_dim, 512, 1024)
+    gm, om = build_pair(c, wdt)
+    gm.set_option(L.OPT_PREFILL_ATTN, attn)
+    assert gm.get_option(L.OPT_PREFILL_ATTN) == attn
+    toks = [1] + [3 + (i * 37) % 500 for i in range(899)]
+    st = InferenceState(c)
+    gm.prefill(toks[:600], 0, st)
+    gm.prefill(toks[600:], 600, st)
+    for pos, tok in enumerate(toks):
+        om.forward(tok, pos, L.OUTPUT_LOGITS if pos == len(toks) - 1 else L.HYDRATE_KV_CACHE)
+    ref = om.logits()
+    got = st.logits()
+    assert np.abs(got - ref).max() <= bar(ref), float(np.abs(got - ref).max())
+    for layer in range(c.n_layers):
+        for which in (0, 1):
+            a = f16(gm.kv_read(layer, which, 0, len(toks)))
+            b = f16(om.kv(layer, which)[:len(toks)])
+            assert np.abs(a - b).max() <= 2e-3 * max(1.0, np.abs(b).max()), (layer, which)

@@ -582,4 +582,168 @@ __global__ __launch_bounds__(ATTN_THREADS) void prefill_attn_kernel(AttnArgs a, 
     attn_block<HD, QPK, ATTN_THREADS, false>(a, blockIdx.x, blockIdx.y, smem, nullptr);
 }
 
+// ---- causal attention of a prompt pass on MFMA ------------------------------------------
+// Per token and head (src/infer.cpp:279-301 / :338): s_t = (q . K[t]) * (1/sqrtf(hd)) over slots
+// [0, pos], p = softmax(s) (max-subtract, expf), out = sum_t p_t V[t].  Computed flash-style
+// over 32-slot tiles with a running max and sum (f32), the sum divided out at the end.
+// One wave = one KV head x 32 query rows (32/QPK tokens x the QPK heads sharing that KV head).
+//   S^T = K Q^T on v_mfma_f32_32x32x16_f16: A = K rows (exact f16), B = q split into exact
+//         f16 hi + lo under a power-of-two row scale (as prefill_split_kernel; <= 2^-22 |q|),
+//         two MFMAs per 16-wide k step, products exact in f32.  D: lane (h, row j) holds the
+//         16 slots (r & 3) + 8 (r >> 2) + 4 h of query row j, so the row's max / sum is one
+//         lane pair (l, l ^ 32) and the rescale of O is a per-lane scalar.
+//   O^T = V^T P^T: B = p (this lane's own 16 values, as f16 hi + lo: |p - hi - lo| <= 2^-25),
+//         A = V^T fragments from a transposed LDS copy of the V tile; the k index of MFMA step
+//         s, lane half h, element e is slot 16 s + 8 (e >> 2) + 4 h + (e & 3) on both sides.
+// grid (n_kv_heads, ceil(n / (32/QPK))), 64 threads; no ring wrap inside a pass (pf_supported)
+template <int HD, int QPK>
+__global__ __launch_bounds__(64) void prefill_fa_kernel(const float* q, const uint16_t* kc, const uint16_t* vc,
+                                                         float* out, int n, int pos0, int q_stride, int kv_dim) {
+    constexpr int TPW = 32 / QPK;        // tokens per wave
+    constexpr int KS = HD / 16;          // k steps of q . k
+    constexpr int NDT = (HD + 31) / 32;  // 32-row d tiles of O^T
+    constexpr int VP = 40;               // V^T row pitch (f16): conflict-free 8-byte fragment reads
+    static_assert(HD % 16 == 0 && 32 % QPK == 0, "prefill_fa_kernel: head shape");
+    __shared__ __attribute__((aligned(16))) uint16_t vt[NDT * 32 * VP];
+    const int lane = threadIdx.x, j32 = lane & 31, h = lane >> 5;
+    const int g = blockIdx.x;
+    const int t0 = (gridDim.y - 1 - blockIdx.y) * TPW;  // longest rows first
+    const int tq = t0 + j32 / QPK;
+    const int tqc = min(tq, n - 1);
+    const int pos = pos0 + tqc;
+    const int head = g * QPK + j32 % QPK;
+    const int last = pos0 + min(t0 + TPW, n) - 1;  // the wave's last slot
+    const float scale = 1.0f / sqrtf((float)HD);  // src/infer.cpp:338
+    // q row, split: this lane's k = 16 ks + 8 h + e
+    f16x8 qh[KS], ql[KS];
+    float inv_s;
+    {
+        const float* qr = q + (size_t)tqc * q_stride + (size_t)head * HD;
+        float v[KS][8];
+        float mx = 0.f;
+#pragma unroll
+        for (int ks = 0; ks < KS; ks++) {
+            const float4 a = *(const float4*)(qr + 16 * ks + 8 * h), b = *(const float4*)(qr + 16 * ks + 8 * h + 4);
+            v[ks][0] = a.x; v[ks][1] = a.y; v[ks][2] = a.z; v[ks][3] = a.w;
+            v[ks][4] = b.x; v[ks][5] = b.y; v[ks][6] = b.z; v[ks][7] = b.w;
+#pragma unroll
+            for (int e = 0; e < 8; e++) mx = fmaxf(mx, fabsf(v[ks][e]));
+        }
+        mx = fmaxf(mx, __shfl_xor(mx, 32));
+        int ex = 0;
+        const bool ok = mx > 0.f && mx <= FLT_MAX;
+        if (ok) frexpf(mx, &ex);
+        const float sc = ok ? ldexpf(1.f, 15 - ex) : 1.f;
+        inv_s = 1.f / sc;
+#pragma unroll
+        for (int ks = 0; ks < KS; ks++)
+#pragma unroll
+            for (int e = 0; e < 8; e++) {
+                const float u = v[ks][e] * sc;
+                qh[ks][e] = (_Float16)u;
+                ql[ks][e] = (_Float16)(u - (float)qh[ks][e]);
+            }
+    }
+    if (HD < 32) {  // rows d >= HD of the single d tile read as zero
+        for (int i = lane; i < (32 - HD) * VP / 2; i += 64) ((uint32_t*)(vt + HD * VP))[i] = 0u;
+    }
+    f32x16 o[NDT];
+#pragma unroll
+    for (int dt = 0; dt < NDT; dt++) o[dt] = f32x16{};
+    float m = -INFINITY, lsum = 0.f;
+    const uint16_t* kg = kc + (size_t)g * HD;
+    const uint16_t* vg = vc + (size_t)g * HD;
+    constexpr int VCH = 16 * HD / 8;  // (slot pair, 8 d) chunks of a V tile
+    constexpr int VIT = (VCH + 63) / 64;
+    for (int b = 0; b <= last; b += 32) {
+        // V tile -> registers (zeros past the wave's last slot: garbage x p = 0 could be NaN)
+        u32x4 va[VIT], vb[VIT];
+#pragma unroll
+        for (int it = 0; it < VIT; it++) {
+            const int c = lane + 64 * it, sp = c & 15, d8 = c >> 4;
+            const int s0 = b + 2 * sp;
+            va[it] = vb[it] = u32x4{0u, 0u, 0u, 0u};
+            if (c < VCH) {
+                if (s0 <= last) va[it] = *(const u32x4*)(vg + (size_t)s0 * kv_dim + 8 * d8);
+                if (s0 + 1 <= last) vb[it] = *(const u32x4*)(vg + (size_t)(s0 + 1) * kv_dim + 8 * d8);
+            }
+        }
+        // S^T = K Q^T (K rows clamped to the wave's range; masked below)
+        f32x16 st = f32x16{};
+        {
+            const uint16_t* kr = kg + (size_t)min(b + j32, last) * kv_dim + 8 * h;
+#pragma unroll
+            for (int ks = 0; ks < KS; ks++) {
+                const f16x8 kf = __builtin_bit_cast(f16x8, *(const u32x4*)(kr + 16 * ks));
+                st = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf, qh[ks], st, 0, 0, 0);
+                st = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf, ql[ks], st, 0, 0, 0);
+            }
+        }
+        __syncthreads();  // the previous tile's V^T reads are done
+#pragma unroll
+        for (int it = 0; it < VIT; it++) {
+            const int c = lane + 64 * it, sp = c & 15, d8 = c >> 4;
+            if (c < VCH) {
+#pragma unroll
+                for (int e = 0; e < 8; e++) {
+                    const uint32_t lo = (va[it][e >> 1] >> (16 * (e & 1))) & 0xffffu;
+                    const uint32_t hi = (vb[it][e >> 1] >> (16 * (e & 1))) & 0xffffu;
+                    *(uint32_t*)(vt + (8 * d8 + e) * VP + 2 * sp) = lo | (hi << 16);
+                }
+            }
+        }
+        // online softmax over this lane's 16 slots and its partner's
+        float sv[16];
+        float tm = -INFINITY;
+#pragma unroll
+        for (int r = 0; r < 16; r++) {
+            const int slot = b + (r & 3) + 8 * (r >> 2) + 4 * h;
+            sv[r] = slot <= pos ? st[r] * inv_s * scale : -INFINITY;
+            tm = fmaxf(tm, sv[r]);
+        }
+        tm = fmaxf(tm, __shfl_xor(tm, 32));
+        const float mn = fmaxf(m, tm);  // finite: slot 0 <= pos on the first tile
+        const float alpha = expf(m - mn);
+        m = mn;
+        float ps = 0.f;
+        f16x8 ph[2], pl[2];
+#pragma unroll
+        for (int r = 0; r < 16; r++) {
+            const float p = expf(sv[r] - mn);
+            ps += p;
+            const _Float16 hi = (_Float16)p;
+            ph[r >> 3][r & 7] = hi;
+            pl[r >> 3][r & 7] = (_Float16)(p - (float)hi);
+        }
+        lsum = lsum * alpha + ps;
+#pragma unroll
+        for (int dt = 0; dt < NDT; dt++) o[dt] *= alpha;
+        __syncthreads();  // V^T tile written
+#pragma unroll
+        for (int s2 = 0; s2 < 2; s2++) {
+#pragma unroll
+            for (int dt = 0; dt < NDT; dt++) {
+                const uint16_t* vr = vt + (32 * dt + j32) * VP + 16 * s2 + 4 * h;
+                const uint2 x0 = *(const uint2*)vr, x1 = *(const uint2*)(vr + 8);
+                const f16x8 vf = __builtin_bit_cast(f16x8, u32x4{x0.x, x0.y, x1.x, x1.y});
+                o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vf, ph[s2], o[dt], 0, 0, 0);
+                o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vf, pl[s2], o[dt], 0, 0, 0);
+            }
+        }
+    }
+    const float l = lsum + __shfl_xor(lsum, 32);
+    if (tq >= n) return;
+    const float inv_l = 1.f / l;
+    float* orow = out + (size_t)tq * q_stride + (size_t)head * HD;
+#pragma unroll
+    for (int dt = 0; dt < NDT; dt++)
+#pragma unroll
+        for (int r = 0; r < 16; r += 4) {
+            const int d = 32 * dt + 8 * (r >> 2) + 4 * h;
+            if (d < HD)
+                *(float4*)(orow + d) =
+                    float4{o[dt][r] * inv_l, o[dt][r + 1] * inv_l, o[dt][r + 2] * inv_l, o[dt][r + 3] * inv_l};
+        }
+}
+
 }  // namespace xalm

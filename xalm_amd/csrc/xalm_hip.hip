@@ -137,6 +137,7 @@ struct xh_ctx {
     std::map<std::vector<int>, BlasPlan> blas_plans;
     bool pf_split_ready = false;                 // pf_norm left the next GEMM's split input
     bool pf_glu_split = true;                    // XH_OPT_PREFILL_GLU_SPLIT: fused GLU -> split input
+    bool pf_attn_mfma = true;                    // XH_OPT_PREFILL_ATTN: 1 MFMA tiles, 0 per-token split kernel
     bool pf_alloc = false;
     // T = PF_TOK_MAX tokens (the largest pass)
     uint16_t* pf_xh = nullptr;                   // [2T][max K] f16 halves of a GEMM input (pf_alloc)
@@ -884,8 +885,22 @@ void pf_attn_t(xh_ctx* ctx, const AttnArgs& a, int n) {
     hipLaunchKernelGGL(k, dim3(ctx->c.n_kv_heads, a.nsplit, n), dim3(ATTN_THREADS), smem, ctx->stream, a,
                        (const StepParams*)ctx->pf_sp, ctx->q_dim, ctx->c.n_kv_heads);
 }
-bool pf_attn(xh_ctx* ctx, const AttnArgs& a, int n) {
+template <int HD, int QPK>
+void pf_fa_t(xh_ctx* ctx, const AttnArgs& a, int n, int pos0) {
+    constexpr int TPW = 32 / QPK;
+    hipLaunchKernelGGL((prefill_fa_kernel<HD, QPK>), dim3(ctx->c.n_kv_heads, (n + TPW - 1) / TPW), dim3(64), 0,
+                       ctx->stream, a.q, a.kc, a.vc, a.out, n, pos0, ctx->q_dim, ctx->kv_dim);
+}
+bool pf_attn(xh_ctx* ctx, const AttnArgs& a, int n, int pos0) {
     const int hd = ctx->c.head_dim, qpk = ctx->qpk;
+    if (ctx->pf_attn_mfma) {
+        if (hd == 128 && qpk == 4) pf_fa_t<128, 4>(ctx, a, n, pos0);
+        else if (hd == 128 && qpk == 8) pf_fa_t<128, 8>(ctx, a, n, pos0);
+        else if (hd == 64 && qpk == 4) pf_fa_t<64, 4>(ctx, a, n, pos0);
+        else if (hd == 16 && qpk == 2) pf_fa_t<16, 2>(ctx, a, n, pos0);
+        else return false;
+        return true;
+    }
     if (hd == 128 && qpk == 4) pf_attn_t<128, 4>(ctx, a, n);
     else if (hd == 128 && qpk == 8) pf_attn_t<128, 8>(ctx, a, n);
     else if (hd == 64 && qpk == 4) pf_attn_t<64, 4>(ctx, a, n);
@@ -958,7 +973,7 @@ int prefill_batched(xh_ctx* ctx, const int* tokens, int n, int pos0, int want_lo
             // splits for this pass's longest row (attn_block: >= ATTN_MIN_T slots per split)
             aa.counters = ctx->pf_cnt;
             aa.nsplit = std::min(ctx->nsplit, std::max(1, (p0 + m + ATTN_MIN_T - 1) / ATTN_MIN_T));
-            if (!pf_attn(ctx, aa, m)) return set_err(ctx, XH_E_INVALID, "prefill: head shape not instantiated");
+            if (!pf_attn(ctx, aa, m, p0)) return set_err(ctx, XH_E_INVALID, "prefill: head shape not instantiated");
             if ((rc = pf_gemm(ctx, "wo", kdt(w.wo_dt, w.wo_x), w.wo, ctx->q_dim, c.dim, ctx->pf_att, m, ks))) return rc;
             e = PfEpiArgs{};
             e.ks = ks; e.n = m; e.rows = c.dim; e.epi = EPI_RESID; e.out = ctx->pf_x;
@@ -1725,6 +1740,7 @@ int xh_get_option(const xh_ctx* ctx, int option, int* value) {
         case XH_OPT_FUSE_ATTN_WO: *value = ctx->fuse_attn_wo ? 1 : 0; return 0;
         case XH_OPT_PREFILL: *value = ctx->prefill_batched ? ctx->prefill_gemm : 0; return 0;
         case XH_OPT_PREFILL_GLU_SPLIT: *value = ctx->pf_glu_split ? 1 : 0; return 0;
+        case XH_OPT_PREFILL_ATTN: *value = ctx->pf_attn_mfma ? 1 : 0; return 0;
         default: return XH_E_INVALID;
     }
 }
@@ -1745,6 +1761,10 @@ int xh_set_option(xh_ctx* ctx, int option, int value) {
         case XH_OPT_PREFILL_GLU_SPLIT:
             if (value < 0 || value > 1) return set_err(ctx, XH_E_INVALID, "XH_OPT_PREFILL_GLU_SPLIT: 0 or 1");
             ctx->pf_glu_split = value != 0;
+            return 0;
+        case XH_OPT_PREFILL_ATTN:
+            if (value < 0 || value > 1) return set_err(ctx, XH_E_INVALID, "XH_OPT_PREFILL_ATTN: 0 or 1");
+            ctx->pf_attn_mfma = value != 0;
             return 0;
         default: return set_err(ctx, XH_E_INVALID, "unknown option %d", option);
     }
