@@ -9,7 +9,7 @@ import numpy as np
 import pytest
 
 import bench
-from bars import check
+from bars import check, check_logp
 from conftest import fixture_path
 from oracle import oracle as O
 from xalm_amd import _lib as L
@@ -53,8 +53,8 @@ def test_matmul_blocks(dtype, n, d):
 @pytest.mark.parametrize("name", ["tiny_mistral_q8_0", "tiny_mistral_q4_0", "small_llama_q8_0"])
 @pytest.mark.parametrize("fuse", [1, 0])
 def test_forward_on_converter_blocks(name, fuse):
-    # every fixture position with logits vs the oracle (the MFMA prefill does not take block
-    # formats: the token loop)
+    # every fixture position with logits vs the oracle, then the batched prompt path (f32-input
+    # MFMA GEMMs decoding the blocks, prefill.h) and the device greedy loop
     xf = XalmFile(fixture_path(name + ".xalm"))
     gm = Model.from_xalm(xf)
     gm.set_option(L.OPT_FUSE_ATTN_WO, fuse)
@@ -65,13 +65,13 @@ def test_forward_on_converter_blocks(name, fuse):
         gm.forward(st, tok, pos)
         om.forward(tok, pos)
         check(st.logits(), om.logits(), name, "loop", pos)
-    # prompt path (token loop) and the device greedy loop
+    # prompt path and the device greedy loop
     gm.reset()
     om.reset()
     gm.prefill(toks[:9], 0, st)
     for pos, tok in enumerate(toks[:9]):
         om.forward(tok, pos, L.OUTPUT_LOGITS if pos == 8 else L.HYDRATE_KV_CACHE)
-    check(st.logits(), om.logits(), name, "loop")
+    check(st.logits(), om.logits(), name, "prefill")
     out = gm.decode_greedy(9, 6)
     pos = 9
     for t in out:
@@ -116,3 +116,39 @@ def test_block_upload_checks():
         gm.upload(L.WQ, 0, L.Q8_0, raw[:-1])
     gm.upload(L.WQ, 0, L.Q8_0, raw)
     gm.close()
+
+
+@pytest.mark.parametrize("name", ["tiny_mistral_q8_0", "tiny_mistral_q4_0", "small_llama_q8_0"])
+@pytest.mark.parametrize("batched", [1, 0])
+def test_block_prompt_passes(name, batched):
+    """A 100-token prompt (a full 64-token pass + 36) through the batched path on gguf blocks
+    (XH_OPT_PREFILL 1) and the token loop (0) vs the oracle's HYDRATE loop: last logits, every
+    K/V row; then the perplexity path over 80 tokens (lm_head GEMM over block rows)."""
+    xf = XalmFile(fixture_path(name + ".xalm"))
+    gm = Model.from_xalm(xf, context=256)
+    gm.set_option(L.OPT_PREFILL, batched)
+    om = O.OracleModel.from_xalm(xf, context=256)
+    toks = [1] + [3 + (i * 41) % (gm.config.vocab_size - 3) for i in range(99)]
+    st = InferenceState(gm.config)
+    gm.prefill(toks, 0, st)
+    for pos, tok in enumerate(toks):
+        om.forward(tok, pos, L.OUTPUT_LOGITS if pos == len(toks) - 1 else L.HYDRATE_KV_CACHE)
+    check(st.logits(), om.logits(), name, "prefill" if batched else "loop")
+    for layer in range(gm.config.n_layers):
+        for which in (0, 1):
+            a = gm.kv_read(layer, which, 0, len(toks)).view(np.float16).astype(np.float32)
+            b = om.kv(layer, which)[:len(toks)].view(np.float16).astype(np.float32)
+            assert np.abs(a - b).max() <= 2e-3 * max(1.0, np.abs(b).max()), (layer, which)
+    gm.close()
+    gm2 = Model.from_xalm(xf, context=256)
+    gm2.set_option(L.OPT_PREFILL, batched)
+    om2 = O.OracleModel.from_xalm(xf, context=256)
+    got = gm2.token_probs(toks[:80])
+    for pos in range(79):
+        om2.forward(toks[pos], pos)
+        lg = om2.logits()
+        ref = O.sample_prob(lg, toks[pos + 1])
+        if ref < 1e-30:
+            assert got[pos] < 1e-30
+            continue
+        check_logp(float(abs(np.log(got[pos]) - np.log(ref))), lg, name, pos)

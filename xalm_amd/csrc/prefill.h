@@ -46,10 +46,13 @@ struct PfGemmArgs {
 
 // PIPE: K slice a multiple of 4 chunk pairs (weights requested 4 pairs ahead).  RT: 32-row
 // tiles per wave; each X operand load feeds RT x 2 accumulator tiles.
+// gguf blocks (Q8_0 / Q4_0): each lane's 16-B chunk lies in one 32-element block; its f16 d
+// (the planar row's scale area) multiplies the decoded codes, w = q * d exact in f32 as
+// quants.py's dequantize (oracle xo_gq_elem), before the MFMA.
 template <int DT, bool PIPE, int RT>
 __global__ __launch_bounds__(PF_THREADS) void prefill_gemm_kernel(const PfGemmArgs a) {
     constexpr int E = WDec<DT>::E;
-    constexpr int ESZ = 16 / E;  // bytes per element
+    constexpr bool GQ = gq_dt(DT);
     const int lane = threadIdx.x & 63;
     const int gw = blockIdx.x * PF_WAVES + (threadIdx.x >> 6);
     const int n_rt = (a.rows + 32 * RT - 1) / (32 * RT);
@@ -73,12 +76,17 @@ __global__ __launch_bounds__(PF_THREADS) void prefill_gemm_kernel(const PfGemmAr
     // one's 2 E RT MFMAs run (weights come from HBM, X from L2)
     struct Stage {
         u32x4 w[RT];
+        float d[RT];
         float4 x0[E / 4], x1[E / 4];
     };
+    const size_t qb = GQ ? gq_qbytes(DT, (size_t)a.K) : 0;
     auto load = [&](Stage& st, const int kb) {
         const int k = kb + E * h;
 #pragma unroll
-        for (int i = 0; i < RT; i++) st.w[i] = *(const u32x4*)(wrow[i] + (size_t)k * ESZ);
+        for (int i = 0; i < RT; i++) {
+            st.w[i] = *(const u32x4*)(wrow[i] + (size_t)k * 16 / E);
+            if constexpr (GQ) st.d[i] = f16_bits_to_f32(*(const uint16_t*)(wrow[i] + qb + (size_t)(k >> 5) * 2));
+        }
 #pragma unroll
         for (int q = 0; q < E / 4; q++) st.x0[q] = *(const float4*)(x0 + k + 4 * q);
         if (n_tt > 1) {
@@ -91,6 +99,10 @@ __global__ __launch_bounds__(PF_THREADS) void prefill_gemm_kernel(const PfGemmAr
         for (int i = 0; i < RT; i++) {
             float wf[E];
             WDec<DT>::dec(st.w[i], wf);
+            if constexpr (GQ) {
+#pragma unroll
+                for (int e = 0; e < E; e++) wf[e] *= st.d[i];
+            }
 #pragma unroll
             for (int q = 0; q < E / 4; q++) {
                 acc0[i] = __builtin_amdgcn_mfma_f32_32x32x2f32(st.x0[q].x, wf[4 * q + 0], acc0[i], 0, 0, 0);

@@ -131,9 +131,11 @@ struct xh_ctx {
     struct BlasPlan {
         hipblasLtMatmulDesc_t md = nullptr;
         hipblasLtMatrixLayout_t la = nullptr, lb = nullptr, lc = nullptr;
-        hipblasLtMatmulAlgo_t algo{};
+        std::vector<hipblasLtMatmulAlgo_t> cands;  // the heuristic's candidates (empty: none)
+        int chosen = -1;                            // -1 until the first GEMM
         bool ready = false;
     };
+    int blas_ok[2] = {0, 0};  // f16, e4m3: 0 unprobed, 1 every shape of the model has a plan, -1 not
     std::map<std::vector<int>, BlasPlan> blas_plans;
     bool pf_split_ready = false;                 // pf_norm left the next GEMM's split input
     bool pf_glu_split = true;                    // XH_OPT_PREFILL_GLU_SPLIT: fused GLU -> split input
@@ -677,11 +679,14 @@ int pf_alloc(xh_ctx* ctx) {
             return set_err((ctx), XH_E_HIP, "%s failed: hipBLASLt status %d", #expr, (int)_s);       \
     } while (0)
 
-// Y[n][rows] (f32) = X[n][K] (f16) . W[rows][K]^T on hipBLASLt.  Column-major view: D (rows x n,
-// ld rows) = op(A) B with A = W stored K x rows (ld K, transposed), B = X stored K x n (ld K).
-// f16 weights: f32 compute; e4m3 weights: f32 accumulation over f16 products (FAST_16F; e4m3 is
-// exact in f16).  One plan per (dtype, rows, K, n), algorithm = the heuristic's first.
-int blas_gemm(xh_ctx* ctx, int dt, const void* w, int K, int rows, const uint16_t* x, int n, float* y) {
+// Plan of Y[n][rows] (f32) = X[n][K] (f16) . W[rows][K]^T on hipBLASLt.  Column-major view:
+// D (rows x n, ld rows) = op(A) B with A = W stored K x rows (ld K, transposed), B = X stored
+// K x n (ld K).  f16 weights: f32 compute; e4m3 weights: f32 accumulation over f16 products
+// (FAST_16F; e4m3 is exact in f16).  One plan per (dtype, rows, K, n) holding the heuristic's
+// candidates; *plan = nullptr when the library has none (the torch-bundled hipBLASLt, loaded
+// first under the same soname in a process that imported torch, has no e4m3 kernels here).
+int blas_plan(xh_ctx* ctx, int dt, int rows, int K, int n, xh_ctx::BlasPlan** plan) {
+    *plan = nullptr;
     if (!ctx->blas) {
         BLAS_TRY(ctx, hipblasLtCreate(&ctx->blas));
         char* ws = nullptr;
@@ -705,25 +710,62 @@ int blas_gemm(xh_ctx* ctx, int dt, const void* w, int K, int rows, const uint16_
         hipblasLtMatmulPreference_t pref;
         BLAS_TRY(ctx, hipblasLtMatmulPreferenceCreate(&pref));
         size_t wss = PF_BLAS_WS;
-        hipblasLtMatmulHeuristicResult_t heur[1];
+        constexpr int NH = 8;
+        hipblasLtMatmulHeuristicResult_t heur[NH];
         int nret = 0;
         hipblasStatus_t st = hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES,
                                                                    &wss, sizeof wss);
         if (st == HIPBLAS_STATUS_SUCCESS)
-            st = hipblasLtMatmulAlgoGetHeuristic(ctx->blas, p.md, p.la, p.lb, p.lc, p.lc, pref, 1, heur, &nret);
+            st = hipblasLtMatmulAlgoGetHeuristic(ctx->blas, p.md, p.la, p.lb, p.lc, p.lc, pref, NH, heur, &nret);
         hipblasLtMatmulPreferenceDestroy(pref);
-        if (st != HIPBLAS_STATUS_SUCCESS || nret < 1)
-            return set_err(ctx, XH_E_HIP, "hipBLASLt: no algorithm for %d x %d x %d (dtype %d), status %d", rows, K, n,
-                           dt, (int)st);
-        p.algo = heur[0].algo;
+        for (int i = 0; st == HIPBLAS_STATUS_SUCCESS && i < nret; i++) p.cands.push_back(heur[i].algo);
         p.ready = true;
         it = ctx->blas_plans.find(key);
     }
-    const xh_ctx::BlasPlan& p = it->second;
-    if (!p.ready) return set_err(ctx, XH_E_HIP, "hipBLASLt: plan %d x %d x %d failed earlier", rows, K, n);
+    if (!it->second.ready) return set_err(ctx, XH_E_HIP, "hipBLASLt: plan %d x %d x %d failed earlier", rows, K, n);
+    if (!it->second.cands.empty()) *plan = &it->second;
+    return 0;
+}
+
+// the GEMM; a full pass (n = 2 PF_TOK_BLAS) first picks the fastest candidate on this very
+// GEMM (its output is rewritten by the real call); other passes take the first candidate
+int blas_gemm(xh_ctx* ctx, int dt, const void* w, int K, int rows, const uint16_t* x, int n, float* y) {
+    xh_ctx::BlasPlan* pp = nullptr;
+    int rc = blas_plan(ctx, dt, rows, K, n, &pp);
+    if (rc) return rc;
+    if (!pp) return set_err(ctx, XH_E_HIP, "hipBLASLt: no algorithm for %d x %d x %d (dtype %d)", rows, K, n, dt);
+    xh_ctx::BlasPlan& p = *pp;
     const float alpha = 1.f, beta = 0.f;
-    BLAS_TRY(ctx, hipblasLtMatmul(ctx->blas, p.md, &alpha, w, p.la, x, p.lb, &beta, y, p.lc, y, p.lc, &p.algo,
-                                  ctx->blas_ws, PF_BLAS_WS, ctx->stream));
+    if (p.chosen < 0) {
+        p.chosen = 0;
+        if (n == 2 * PF_TOK_BLAS && p.cands.size() > 1) {
+            HIP_TRY(ctx, hipGetLastError());  // an earlier launch's error is reported as such
+            hipEvent_t e0, e1;
+            HIP_TRY(ctx, hipEventCreate(&e0));
+            HIP_TRY(ctx, hipEventCreate(&e1));
+            float best = FLT_MAX;
+            for (size_t i = 0; i < p.cands.size(); i++) {
+                float ms = 0.f;
+                bool ok = hipblasLtMatmul(ctx->blas, p.md, &alpha, w, p.la, x, p.lb, &beta, y, p.lc, y, p.lc,
+                                          &p.cands[i], ctx->blas_ws, PF_BLAS_WS, ctx->stream) == HIPBLAS_STATUS_SUCCESS;
+                ok = ok && hipEventRecord(e0, ctx->stream) == hipSuccess;
+                for (int r = 0; ok && r < 3; r++)
+                    ok = hipblasLtMatmul(ctx->blas, p.md, &alpha, w, p.la, x, p.lb, &beta, y, p.lc, y, p.lc,
+                                         &p.cands[i], ctx->blas_ws, PF_BLAS_WS, ctx->stream) == HIPBLAS_STATUS_SUCCESS;
+                ok = ok && hipEventRecord(e1, ctx->stream) == hipSuccess && hipEventSynchronize(e1) == hipSuccess &&
+                     hipEventElapsedTime(&ms, e0, e1) == hipSuccess;
+                if (ok && ms < best) {
+                    best = ms;
+                    p.chosen = (int)i;
+                }
+            }
+            (void)hipGetLastError();  // a candidate that failed to launch is skipped, not reported
+            hipEventDestroy(e0);
+            hipEventDestroy(e1);
+        }
+    }
+    BLAS_TRY(ctx, hipblasLtMatmul(ctx->blas, p.md, &alpha, w, p.la, x, p.lb, &beta, y, p.lc, y, p.lc,
+                                  &p.cands[p.chosen], ctx->blas_ws, PF_BLAS_WS, ctx->stream));
     return 0;
 }
 
@@ -763,9 +805,46 @@ void pf_gemm16_t(const PfGemm16Args& a, hipStream_t s) {
     hipLaunchKernelGGL((prefill_gemm16_kernel<DT, PF_RT16>), dim3((waves + PF_WAVES - 1) / PF_WAVES), dim3(PF_THREADS),
                        0, s, a);
 }
+// weights per 16-byte chunk of the f32-input MFMA kernel's decoders (WDec<DT>::E)
+int pf_elems(int dt) {
+    if (dt == XH_F8_E4M3_EXACT || dt == XH_F8_E5M2_EXACT || dt == XH_Q8_0) return 16;
+    return dt == XH_Q4_0 ? 32 : elems_per_16b(dt);
+}
 // XH_OPT_PREFILL 1: hipBLASLt runs the GEMM over weights of dtype dt (f16, or e4m3 whose codes
 // all convert exactly in hardware: kdt keeps the _EXACT dtypes off this path)
-bool pf_blas(const xh_ctx* ctx, int dt) { return ctx->prefill_gemm == 1 && (dt == XH_F16 || dt == XH_F8_E4M3); }
+bool pf_blas(const xh_ctx* ctx, int dt) {
+    if (ctx->prefill_gemm != 1 || (dt != XH_F16 && dt != XH_F8_E4M3)) return false;
+    return ctx->blas_ok[dt == XH_F8_E4M3] > 0;
+}
+// Once per context: does hipBLASLt have a plan for every full-pass GEMM of the model with each
+// eligible dtype?  (A dtype without one keeps the MFMA kernels: XH_OPT_PREFILL 1's fallback.)
+int pf_blas_probe(xh_ctx* ctx) {
+    if (ctx->prefill_gemm != 1) return 0;
+    const xh_config& c = ctx->c;
+    struct G { int dt, rows, K; };
+    std::vector<G> gs;
+    for (const LayerW& w : ctx->L) {
+        gs.push_back({kdt(w.qkv_dt, w.qkv_x), ctx->q_dim + 2 * ctx->kv_dim, c.dim});
+        gs.push_back({kdt(w.wo_dt, w.wo_x), c.dim, ctx->q_dim});
+        gs.push_back({kdt(w.w13_dt, w.w13_x), 2 * c.hidden_dim, c.dim});
+        gs.push_back({kdt(w.w2_dt, w.w2_x), c.dim, c.hidden_dim});
+    }
+    gs.push_back({kdt(ctx->wcls_dt, ctx->wcls_x), std::min(PF_CLS_CHUNK, c.vocab_size), c.dim});
+    for (int f8 = 0; f8 < 2; f8++) {
+        if (ctx->blas_ok[f8]) continue;
+        const int dt = f8 ? XH_F8_E4M3 : XH_F16;
+        int ok = 1;
+        for (const G& g : gs) {
+            if (g.dt != dt) continue;
+            xh_ctx::BlasPlan* p = nullptr;
+            int rc = blas_plan(ctx, dt, g.rows, g.K, 2 * PF_TOK_BLAS, &p);
+            if (rc) return rc;
+            if (!p) ok = -1;
+        }
+        ctx->blas_ok[f8] = ok;
+    }
+    return 0;
+}
 // Layout of the split-f16 input of the GEMM over W (dtype dt, [rows][K]): 0 = row-major (the
 // hipBLASLt path), E > 0 = the split-f16 kernel's fragments, -1 = no split (f32-input MFMA).
 // XH_OPT_PREFILL 1: hipBLASLt for f16 / e4m3, the split kernel for e5m2; 2: the split kernel
@@ -843,11 +922,11 @@ int pf_gemm(xh_ctx* ctx, const char* what, int dt, const void* w, int K, int row
         ks = a.ks;
         return 0;
     }
-    const int E = (dt == XH_F8_E4M3_EXACT || dt == XH_F8_E5M2_EXACT) ? 16 : elems_per_16b(dt);
+    const int E = pf_elems(dt);
     if (K % (2 * E) || n > PF_TOK) return set_err(ctx, XH_E_INVALID, "prefill: %s shape not supported", what);
     PfGemmArgs a{};
     a.w = w; a.K = K; a.rows = rows; a.x = x; a.n = n; a.part = ctx->pf_part;
-    a.row_bytes = (size_t)K * (16 / E);
+    a.row_bytes = gq_dt(dt) ? gq_pitch(dt, K) : (size_t)K * (16 / E);
     a.ks = pf_ks(rows, K, E);
     if ((size_t)a.ks * rows > PF_PART_ROWS) return set_err(ctx, XH_E_INVALID, "prefill: %s shape not supported", what);
     hipStream_t s = ctx->stream;
@@ -858,6 +937,8 @@ int pf_gemm(xh_ctx* ctx, const char* what, int dt, const void* w, int K, int row
         case XH_F8_E4M3: pf_gemm_t<XH_F8_E4M3>(a, s); break;
         case XH_F8_E5M2: pf_gemm_t<XH_F8_E5M2>(a, s); break;
         case XH_Q8: pf_gemm_t<XH_Q8>(a, s); break;
+        case XH_Q8_0: pf_gemm_t<XH_Q8_0>(a, s); break;
+        case XH_Q4_0: pf_gemm_t<XH_Q4_0>(a, s); break;
         case XH_F8_E4M3_EXACT: pf_gemm_t<XH_F8_E4M3_EXACT>(a, s); break;
         case XH_F8_E5M2_EXACT: pf_gemm_t<XH_F8_E5M2_EXACT>(a, s); break;
         default: return set_err(ctx, XH_E_INVALID, "prefill: %s dtype %d not supported", what, dt);
@@ -916,11 +997,12 @@ bool pf_supported(const xh_ctx* ctx, int n, int pos0) {
     if (!ctx->prefill_batched || pos0 + n > c.max_seq_len) return false;
     const int hd = c.head_dim, qpk = ctx->qpk;
     if (!((hd == 128 && (qpk == 4 || qpk == 8)) || (hd == 64 && qpk == 4) || (hd == 16 && qpk == 2))) return false;
-    // no GEMM form for the gguf blocks: those models take the token loop
-    if (gq_dt(ctx->wcls_dt)) return false;
+    // every GEMM's K in whole chunk pairs of its decoder (f32-input kernel; the others need less)
+    auto ok = [](int dt, int K) { return K % (2 * pf_elems(dt)) == 0; };
     for (const LayerW& w : ctx->L)
-        if (gq_dt(w.qkv_dt) || gq_dt(w.wo_dt) || gq_dt(w.w13_dt) || gq_dt(w.w2_dt)) return false;
-    return c.dim % 32 == 0 && c.hidden_dim % 32 == 0 && ctx->q_dim % 32 == 0;
+        if (!ok(w.qkv_dt, c.dim) || !ok(w.wo_dt, ctx->q_dim) || !ok(w.w13_dt, c.dim) || !ok(w.w2_dt, c.hidden_dim))
+            return false;
+    return ok(ctx->wcls_dt, c.dim) && c.dim % 32 == 0 && c.hidden_dim % 32 == 0 && ctx->q_dim % 32 == 0;
 }
 
 // tokens[0..n) at positions pos0..: HYDRATE for every token, then the last token's logits.
@@ -936,6 +1018,7 @@ int prefill_batched(xh_ctx* ctx, const int* tokens, int n, int pos0, int want_lo
         ((rc = dmalloc(ctx, &ctx->pf_logits, (size_t)PF_TOK_MAX * c.vocab_size)) ||
          (rc = dmalloc(ctx, &ctx->pf_tgt, (size_t)PF_TOK_MAX))))
         return rc;
+    if ((rc = pf_blas_probe(ctx))) return rc;
     const int pass = ctx->pf_pass = pf_pass_tokens(ctx);
     std::vector<StepParams> sps(pass);
     for (int off = 0; off < n; off += pass) {
