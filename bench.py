@@ -278,7 +278,7 @@ def main():
     ap.add_argument("--kernel-iters", type=int, default=200)
     ap.add_argument("--prefill-mode", type=int, default=1, choices=(1, 2, 3),
                     help="batched prefill GEMMs (XH_OPT_PREFILL): 1 default per dtype (hipBLASLt for f16 / "
-                         "e4m3 weights), 2 split-f16 MFMA wherever the weights allow, 3 f32-input MFMA only")
+                         "fp8 weights), 2 split-f16 MFMA wherever the weights allow, 3 f32-input MFMA only")
     ap.add_argument("--prefill-tokens", type=int, default=2048,
                     help="also time xh_prefill of this many prompt tokens (batched path; 0 = skip)")
     ap.add_argument("--fuse-attn-wo", type=int, default=1, choices=(0, 1),
@@ -361,10 +361,11 @@ def main():
         flops = 2.0 * args.prefill_tokens * c.n_layers * layer_params  # matrix products only
         prefill = {"tokens": args.prefill_tokens, "ms": round(pf_s * 1e3, 2),
                    "tok_s": round(args.prefill_tokens / pf_s, 1),
-                   "mode": {0: "per-token", 1: "batched (hipBLASLt for f16 / e4m3 weights, else MFMA kernels)",
+                   "mode": {0: "per-token", 1: "batched (hipBLASLt for f16 / fp8 weights, else MFMA kernels)",
                             2: "batched split-f16 MFMA", 3: "batched f32-input MFMA"}[model.get_option(L.OPT_PREFILL)],
-                   "note": "f16 / e4m3 weights: passes of 512 tokens, hipBLASLt GEMMs over f16 hi+lo activation "
-                           "pairs (power-of-two row scale, ~22-bit mantissa); other dtypes: passes of 64 tokens on "
+                   "note": "f16 / fp8 weights: passes of 512 tokens, hipBLASLt f16 GEMMs (fp8 matrices through their "
+                           "exact f16 image) over f16 hi+lo activation pairs (power-of-two row scale, ~22-bit "
+                           "mantissa); other dtypes: passes of 64 tokens on "
                            "the hand-written MFMA GEMMs (f32 activations as the reference, or split-f16)",
                    "matmul_tflops": round(flops / pf_s / 1e12, 1)}
         # run_perplexity's loop (xh_perplexity): the same tokens, every token's logits and

@@ -181,10 +181,10 @@ int xh_set_graphs(xh_ctx* ctx, int enable);
 /* Launch-structure variants.  XH_OPT_FUSE_ATTN_WO (default 1): 1 = attention and Wo (+ residual)
  * in one launch with an in-launch hand-off (attn_wo.h); 0 = two launches.  Same math. */
 /* XH_OPT_PREFILL (default 1): xh_prefill / xh_perplexity process the prompt in passes, each
- * weight matrix streamed once per pass into a GEMM (prefill.h).  1 = f16 and e4m3 weights on
- * hipBLASLt in passes of 512 tokens, activations as exact f16 hi + lo pairs under a
- * power-of-two row scale (≈22-bit mantissa, f32 accumulation); e5m2 on the split-f16 MFMA
- * kernel, other dtypes on the f32-input MFMA kernel (activations exactly as the reference),
+ * weight matrix streamed once per pass into a GEMM (prefill.h).  1 = f16 and fp8 weights on
+ * hipBLASLt in passes of 512 tokens (fp8 matrices through their exact f16 image), activations
+ * as exact f16 hi + lo pairs under a power-of-two row scale (≈22-bit mantissa, f32
+ * accumulation); other dtypes on the f32-input MFMA kernel (activations exactly as the reference),
  * passes of 64 tokens when any layer's GEMM is off hipBLASLt; 2 = the split-f16 MFMA kernel
  * wherever the weights convert exactly to f16 (f16, fp8); 3 = f32-input MFMA only; 0 = one
  * forward per token (the reference's loop, src/main.cpp:94-100).  Same math per token up to

@@ -143,7 +143,7 @@ def test_prefill_matches_oracle(name, context, engine):
 @pytest.mark.parametrize("n", [1, 37, 64, 150])
 def test_batched_prefill_matches_oracle(name, n, mode):
     """xh_prefill's batched path (prefill.h: hipBLASLt GEMMs over passes of <= 512 tokens for
-    f16 / e4m3 weights, MFMA GEMMs over passes of <= 64 tokens otherwise; causal attention per
+    f16 / fp8 weights, MFMA GEMMs over passes of <= 64 tokens otherwise; causal attention per
     token) vs the oracle's token-by-token HYDRATE loop: last logits, every
     layer's K and V rows, and the greedy continuation after it.  mode 1: the default choice
     per dtype; 2: split-f16 MFMA wherever the weights allow (f16 / fp8); 3: f32-input MFMA."""
@@ -173,7 +173,7 @@ def test_batched_prefill_matches_oracle(name, n, mode):
 
 @pytest.mark.parametrize("name", ["tiny_mistral_f16", "tiny_mistral_f8_e4m3", "small_llama_f16"])
 def test_blas_prefill_multi_pass_matches_oracle(name):
-    """XH_OPT_PREFILL 1 on f16 / e4m3 weights: hipBLASLt passes of 512 tokens; 700 tokens = a
+    """XH_OPT_PREFILL 1 on f16 / fp8 weights: hipBLASLt passes of 512 tokens; 700 tokens = a
     full pass and a 188-token one (the second attends over the first pass's K/V rows).  Last
     logits and every layer's K/V rows vs the oracle's token loop, then the perplexity path over
     600 tokens (lm_head as one hipBLASLt GEMM per pass, or 64-token slices for bf16 lm_heads)."""
@@ -421,7 +421,7 @@ def check_probs(got, om, toks, fixture=None):
                                   "small_llama_f16"])
 def test_perplexity_probs_match_oracle(name, prefill):
     # xh_perplexity: batched passes (prefill 2 / 3 and bf16: 89 tokens = a full 64-token pass + 25;
-    # prefill 1 on f16 / e4m3: one hipBLASLt pass; lm_head
+    # prefill 1 on f16 / fp8: one hipBLASLt pass; lm_head
     # as one GEMM per pass) and the token loop (prefill 0)
     xf = XalmFile(fixture_path(name + ".xalm"))
     gm = Model.from_xalm(xf, context=256)

@@ -758,4 +758,22 @@ __global__ __launch_bounds__(64) void prefill_fa_kernel(const float* q, const ui
         }
 }
 
+// fp8 weights (e4m3 / e5m2, finite codes only: the _EXACT dtypes never come here) -> f16 bits
+// for the hipBLASLt f16 GEMM of a prompt pass.  Every finite e4m3 / e5m2 value is an f16, so
+// the GEMM multiplies exactly the reference's decoded weights (src/types.h:302-314); the
+// pack's round-toward-zero never rounds.  n16: 16-byte chunks of codes; out: 2 n16 chunks.
+template <int DT>
+__global__ __launch_bounds__(256) void pf_dequant_f16_kernel(const u32x4* w, const size_t n16, u32x4* out) {
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += (size_t)gridDim.x * 256) {
+        const u32x4 v = __builtin_nontemporal_load(w + i);
+        float f[16];
+        WDec<DT>::dec(v, f);
+        uint32_t h[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) h[j] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(f[2 * j], f[2 * j + 1]));
+        out[2 * i] = u32x4{h[0], h[1], h[2], h[3]};
+        out[2 * i + 1] = u32x4{h[4], h[5], h[6], h[7]};
+    }
+}
+
 }  // namespace xalm

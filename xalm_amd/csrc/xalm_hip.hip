@@ -17,8 +17,8 @@
 //   gemv<PRO_RMSNORM, EPI_STORE>    final rmsnorm + lm_head -> logits   (OUTPUT_LOGITS)
 //   gemv<PRO_RMSNORM, EPI_LOGITS>   ... + per-workgroup argmax candidates (greedy graph)
 // fuse_level 0 launches attention and Wo separately.  Prompts go through prefill.h unless
-// XH_OPT_PREFILL is 0: passes of 512 tokens whose GEMMs run on hipBLASLt (f16 / e4m3 weights,
-// split-f16 activations), else passes of 64 tokens on the hand-written MFMA GEMMs.  (Round 2's one-launch engines — persistent,
+// XH_OPT_PREFILL is 0: passes of 512 tokens whose GEMMs run on hipBLASLt (f16 weights, fp8 through
+// their exact f16 image; split-f16 activations), else passes of 64 tokens on the hand-written MFMA GEMMs.  (Round 2's one-launch engines — persistent,
 // LDS-DMA stream, qkv+attention+Wo, column-form attention — measured slower and were removed;
 // DESIGN.md §4.5 / §4.9 keep the measurements.)
 #include <hip/hip_runtime.h>
@@ -120,7 +120,7 @@ struct xh_ctx {
     unsigned* aw_sync = nullptr;
     // batched prefill (prefill.h), buffers allocated on first use
     bool prefill_batched = true;
-    // XH_OPT_PREFILL: 1 = hipBLASLt for f16 / e4m3 weights, the split-f16 MFMA kernel for e5m2,
+    // XH_OPT_PREFILL: 1 = hipBLASLt for f16 / e4m3 / e5m2 weights (fp8 as an exact f16 image),
     // f32 MFMA otherwise; 2 = split-f16 MFMA wherever the weights convert exactly; 3 = f32 MFMA only
     int prefill_gemm = 1;
     int pf_pass = 0;                             // tokens per pass of the current prefill
@@ -135,8 +135,10 @@ struct xh_ctx {
         int chosen = -1;                            // -1 until the first GEMM
         bool ready = false;
     };
-    int blas_ok[2] = {0, 0};  // f16, e4m3: 0 unprobed, 1 every shape of the model has a plan, -1 not
+    int blas_ok = 0;  // 0 unprobed, 1 every GEMM shape of the model has an f16 plan, -1 not
     std::map<std::vector<int>, BlasPlan> blas_plans;
+    uint16_t* pf_wdq = nullptr;                  // f16 image of one fp8 matrix for hipBLASLt (pf_blas_probe)
+    size_t pf_wdq_elems = 0;
     bool pf_split_ready = false;                 // pf_norm left the next GEMM's split input
     bool pf_glu_split = true;                    // XH_OPT_PREFILL_GLU_SPLIT: fused GLU -> split input
     bool pf_attn_mfma = true;                    // XH_OPT_PREFILL_ATTN: 1 MFMA tiles, 0 per-token split kernel
@@ -681,11 +683,11 @@ int pf_alloc(xh_ctx* ctx) {
 
 // Plan of Y[n][rows] (f32) = X[n][K] (f16) . W[rows][K]^T on hipBLASLt.  Column-major view:
 // D (rows x n, ld rows) = op(A) B with A = W stored K x rows (ld K, transposed), B = X stored
-// K x n (ld K).  f16 weights: f32 compute; e4m3 weights: f32 accumulation over f16 products
-// (FAST_16F; e4m3 is exact in f16).  One plan per (dtype, rows, K, n) holding the heuristic's
-// candidates; *plan = nullptr when the library has none (the torch-bundled hipBLASLt, loaded
-// first under the same soname in a process that imported torch, has no e4m3 kernels here).
-int blas_plan(xh_ctx* ctx, int dt, int rows, int K, int n, xh_ctx::BlasPlan** plan) {
+// K x n (ld K); f16 A and B, f32 compute (f16 x f16 products are exact in f32).  fp8 weights
+// reach it as their exact f16 image (pf_dequant): the torch-bundled hipBLASLt, loaded first
+// under the same soname in a process that imported torch, has no e4m3 / e5m2 kernels.  One
+// plan per (rows, K, n) holding the heuristic's candidates; *plan = nullptr when there are none.
+int blas_plan(xh_ctx* ctx, int rows, int K, int n, xh_ctx::BlasPlan** plan) {
     *plan = nullptr;
     if (!ctx->blas) {
         BLAS_TRY(ctx, hipblasLtCreate(&ctx->blas));
@@ -694,17 +696,15 @@ int blas_plan(xh_ctx* ctx, int dt, int rows, int K, int n, xh_ctx::BlasPlan** pl
         if (rc) return rc;
         ctx->blas_ws = ws;
     }
-    const std::vector<int> key{dt, rows, K, n};
+    const std::vector<int> key{rows, K, n};
     auto it = ctx->blas_plans.find(key);
     if (it == ctx->blas_plans.end()) {
         xh_ctx::BlasPlan& p = ctx->blas_plans[key];  // destroyed with the context, even half-built
-        const bool f8 = dt == XH_F8_E4M3;
-        BLAS_TRY(ctx, hipblasLtMatmulDescCreate(&p.md, f8 ? HIPBLAS_COMPUTE_32F_FAST_16F : HIPBLAS_COMPUTE_32F,
-                                                HIP_R_32F));
+        BLAS_TRY(ctx, hipblasLtMatmulDescCreate(&p.md, HIPBLAS_COMPUTE_32F, HIP_R_32F));
         const hipblasOperation_t opT = HIPBLAS_OP_T, opN = HIPBLAS_OP_N;
         BLAS_TRY(ctx, hipblasLtMatmulDescSetAttribute(p.md, HIPBLASLT_MATMUL_DESC_TRANSA, &opT, sizeof opT));
         BLAS_TRY(ctx, hipblasLtMatmulDescSetAttribute(p.md, HIPBLASLT_MATMUL_DESC_TRANSB, &opN, sizeof opN));
-        BLAS_TRY(ctx, hipblasLtMatrixLayoutCreate(&p.la, f8 ? HIP_R_8F_E4M3 : HIP_R_16F, K, rows, K));
+        BLAS_TRY(ctx, hipblasLtMatrixLayoutCreate(&p.la, HIP_R_16F, K, rows, K));
         BLAS_TRY(ctx, hipblasLtMatrixLayoutCreate(&p.lb, HIP_R_16F, K, n, K));
         BLAS_TRY(ctx, hipblasLtMatrixLayoutCreate(&p.lc, HIP_R_32F, rows, n, rows));
         hipblasLtMatmulPreference_t pref;
@@ -729,11 +729,11 @@ int blas_plan(xh_ctx* ctx, int dt, int rows, int K, int n, xh_ctx::BlasPlan** pl
 
 // the GEMM; a full pass (n = 2 PF_TOK_BLAS) first picks the fastest candidate on this very
 // GEMM (its output is rewritten by the real call); other passes take the first candidate
-int blas_gemm(xh_ctx* ctx, int dt, const void* w, int K, int rows, const uint16_t* x, int n, float* y) {
+int blas_gemm(xh_ctx* ctx, const void* w, int K, int rows, const uint16_t* x, int n, float* y) {
     xh_ctx::BlasPlan* pp = nullptr;
-    int rc = blas_plan(ctx, dt, rows, K, n, &pp);
+    int rc = blas_plan(ctx, rows, K, n, &pp);
     if (rc) return rc;
-    if (!pp) return set_err(ctx, XH_E_HIP, "hipBLASLt: no algorithm for %d x %d x %d (dtype %d)", rows, K, n, dt);
+    if (!pp) return set_err(ctx, XH_E_HIP, "hipBLASLt: no algorithm for %d x %d x %d", rows, K, n);
     xh_ctx::BlasPlan& p = *pp;
     const float alpha = 1.f, beta = 0.f;
     if (p.chosen < 0) {
@@ -810,16 +810,19 @@ int pf_elems(int dt) {
     if (dt == XH_F8_E4M3_EXACT || dt == XH_F8_E5M2_EXACT || dt == XH_Q8_0) return 16;
     return dt == XH_Q4_0 ? 32 : elems_per_16b(dt);
 }
-// XH_OPT_PREFILL 1: hipBLASLt runs the GEMM over weights of dtype dt (f16, or e4m3 whose codes
-// all convert exactly in hardware: kdt keeps the _EXACT dtypes off this path)
+// XH_OPT_PREFILL 1: hipBLASLt runs the GEMM over weights of dtype dt: f16 as stored, e4m3 /
+// e5m2 through their exact f16 image (kdt keeps the _EXACT dtypes, whose NaN / Inf codes the
+// reference decodes to finite values, off this path)
 bool pf_blas(const xh_ctx* ctx, int dt) {
-    if (ctx->prefill_gemm != 1 || (dt != XH_F16 && dt != XH_F8_E4M3)) return false;
-    return ctx->blas_ok[dt == XH_F8_E4M3] > 0;
+    if (ctx->prefill_gemm != 1 || (dt != XH_F16 && dt != XH_F8_E4M3 && dt != XH_F8_E5M2)) return false;
+    return ctx->blas_ok > 0;
 }
-// Once per context: does hipBLASLt have a plan for every full-pass GEMM of the model with each
-// eligible dtype?  (A dtype without one keeps the MFMA kernels: XH_OPT_PREFILL 1's fallback.)
+bool pf_f8(int dt) { return dt == XH_F8_E4M3 || dt == XH_F8_E5M2; }
+// Once per context: does hipBLASLt have an f16 plan for every full-pass GEMM of the model?  (If
+// not, every dtype keeps the MFMA kernels: XH_OPT_PREFILL 1's fallback.)  Also sizes the f16
+// image buffer of the largest fp8 matrix.
 int pf_blas_probe(xh_ctx* ctx) {
-    if (ctx->prefill_gemm != 1) return 0;
+    if (ctx->prefill_gemm != 1 || ctx->blas_ok) return 0;
     const xh_config& c = ctx->c;
     struct G { int dt, rows, K; };
     std::vector<G> gs;
@@ -830,25 +833,31 @@ int pf_blas_probe(xh_ctx* ctx) {
         gs.push_back({kdt(w.w2_dt, w.w2_x), c.dim, c.hidden_dim});
     }
     gs.push_back({kdt(ctx->wcls_dt, ctx->wcls_x), std::min(PF_CLS_CHUNK, c.vocab_size), c.dim});
-    for (int f8 = 0; f8 < 2; f8++) {
-        if (ctx->blas_ok[f8]) continue;
-        const int dt = f8 ? XH_F8_E4M3 : XH_F16;
-        int ok = 1;
-        for (const G& g : gs) {
-            if (g.dt != dt) continue;
-            xh_ctx::BlasPlan* p = nullptr;
-            int rc = blas_plan(ctx, dt, g.rows, g.K, 2 * PF_TOK_BLAS, &p);
-            if (rc) return rc;
-            if (!p) ok = -1;
-        }
-        ctx->blas_ok[f8] = ok;
+    int ok = 1;
+    size_t wdq = 0;
+    for (const G& g : gs) {
+        if (g.dt != XH_F16 && !pf_f8(g.dt)) continue;
+        xh_ctx::BlasPlan* p = nullptr;
+        int rc = blas_plan(ctx, g.rows, g.K, 2 * PF_TOK_BLAS, &p);
+        if (rc) return rc;
+        if (!p) ok = -1;
+        if (pf_f8(g.dt)) wdq = std::max(wdq, (size_t)g.rows * g.K);
     }
+    if (ok > 0 && wdq > ctx->pf_wdq_elems) {
+        hipFree(ctx->pf_wdq);
+        ctx->pf_wdq = nullptr;
+        ctx->pf_wdq_elems = 0;
+        int rc = dmalloc(ctx, &ctx->pf_wdq, wdq);
+        if (rc) return rc;
+        ctx->pf_wdq_elems = wdq;
+    }
+    ctx->blas_ok = ok;
     return 0;
 }
 // Layout of the split-f16 input of the GEMM over W (dtype dt, [rows][K]): 0 = row-major (the
 // hipBLASLt path), E > 0 = the split-f16 kernel's fragments, -1 = no split (f32-input MFMA).
-// XH_OPT_PREFILL 1: hipBLASLt for f16 / e4m3, the split kernel for e5m2; 2: the split kernel
-// for f16 and fp8; 3: never split.  The split kernel also needs a K slicing.
+// XH_OPT_PREFILL 1: hipBLASLt for f16 / e4m3 / e5m2 (split kernel for fp8 if hipBLASLt has no
+// plan); 2: the split kernel for f16 and fp8; 3: never split.  The split kernel also needs a K slicing.
 int pf_layout(const xh_ctx* ctx, int dt, int K, int rows) {
     if (pf_blas(ctx, dt)) return 0;
     const bool f8 = dt == XH_F8_E4M3 || dt == XH_F8_E5M2;
@@ -903,7 +912,21 @@ int pf_gemm(xh_ctx* ctx, const char* what, int dt, const void* w, int K, int row
     }
     if (lay == 0) {
         // hi and lo rows as one B operand: partials [2][n][rows], the epilogue scales by 1 / s_t
-        int rc = blas_gemm(ctx, dt, w, K, rows, ctx->pf_xh, 2 * n, ctx->pf_part);
+        if (pf_f8(dt)) {
+            // the matrix's exact f16 image first (one streaming pass: 1 B read, 2 B written per weight)
+            const size_t n16 = (size_t)rows * K / 16;
+            if ((size_t)rows * K > ctx->pf_wdq_elems || K % 16)
+                return set_err(ctx, XH_E_INVALID, "prefill: %s fp8 image does not fit", what);
+            const int grid = (int)std::min<size_t>((n16 + 255) / 256, 8192);
+            if (dt == XH_F8_E4M3)
+                hipLaunchKernelGGL(pf_dequant_f16_kernel<XH_F8_E4M3>, dim3(grid), dim3(256), 0, ctx->stream,
+                                   (const u32x4*)w, n16, (u32x4*)ctx->pf_wdq);
+            else
+                hipLaunchKernelGGL(pf_dequant_f16_kernel<XH_F8_E5M2>, dim3(grid), dim3(256), 0, ctx->stream,
+                                   (const u32x4*)w, n16, (u32x4*)ctx->pf_wdq);
+            w = ctx->pf_wdq;
+        }
+        int rc = blas_gemm(ctx, w, K, rows, ctx->pf_xh, 2 * n, ctx->pf_part);
         if (rc) return rc;
         ctx->pf_scaled = true;
         ks = 2;
@@ -1277,7 +1300,7 @@ void xh_destroy(xh_ctx* ctx) {
     hipFree(ctx->kv); hipFree(ctx->x); hipFree(ctx->q); hipFree(ctx->attn_out); hipFree(ctx->hb);
     hipFree(ctx->logits); hipFree(ctx->part_o); hipFree(ctx->part_ml); hipFree(ctx->attn_cnt); hipFree(ctx->aw_sync); hipFree(ctx->cand); hipFree(ctx->scan_flag);
     hipFree(ctx->pf_tok); hipFree(ctx->pf_x); hipFree(ctx->pf_xn); hipFree(ctx->pf_q); hipFree(ctx->pf_att); hipFree(ctx->pf_h);
-    hipFree(ctx->pf_xh); hipFree(ctx->pf_xl); hipFree(ctx->pf_xs);
+    hipFree(ctx->pf_xh); hipFree(ctx->pf_xl); hipFree(ctx->pf_xs); hipFree(ctx->pf_wdq);
     hipFree(ctx->pf_logits); hipFree(ctx->pf_tgt); hipFree(ctx->ppl_tgt); hipFree(ctx->ppl_prob);
     hipFree(ctx->pf_part); hipFree(ctx->pf_sp); hipFree(ctx->pf_po); hipFree(ctx->pf_pml); hipFree(ctx->pf_cnt); hipFree(ctx->rope_freq);
     hipFree(ctx->aw_trace);
