@@ -34,8 +34,45 @@ __global__ __launch_bounds__(THREADS) void k_round(const AttnArgs a, unsigned* d
 template <int THREADS>
 __global__ __launch_bounds__(THREADS) void k_signal(const AttnArgs a, unsigned* done) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    attn_block<HD, QPK, THREADS, false, false, attn_min_t_partials(HD, THREADS), NoWait, AddArrive, true>(
+    attn_block<HD, QPK, THREADS, false, attn_min_t_partials(HD, THREADS), NoWait, AddArrive, true>(
         a, blockIdx.x / a.nsplit, blockIdx.x % a.nsplit, smem, done);
+}
+
+// diagnostic floor: the split's K rows then V rows (same per-thread addresses as attn_block:
+// 16 lanes per 256-B row slice, ATTN_PREF rows per thread per round) with D rounds in flight,
+// nothing computed but an xor (the memory side of the round loop alone)
+template <int THREADS, int D>
+__global__ __launch_bounds__(THREADS) void k_stream(const AttnArgs a, unsigned* sink) {
+    constexpr int LPR = HD / 8, RPP = THREADS / LPR, STEP = ATTN_PREF * RPP;
+    const int g = blockIdx.x / a.nsplit, s = blockIdx.x % a.nsplit;
+    const int kv_len = a.sp->kv_len;
+    const int T = attn_split_len(kv_len, a.nsplit, attn_min_t_partials(HD, THREADS));
+    const int t0 = s * T, t1 = min(kv_len, t0 + T);
+    if (t0 >= kv_len) return;
+    const int sub = threadIdx.x % LPR, rr = threadIdx.x / LPR;
+    const size_t col = (size_t)g * HD + sub * 8;
+    uint32_t acc = 0;
+    for (int pass = 0; pass < 2; pass++) {
+        const uint16_t* base = pass ? a.vc : a.kc;
+        u32x4 r[D][ATTN_PREF];
+        int nr = (t1 - t0 + STEP - 1) / STEP;
+#pragma unroll
+        for (int d = 0; d < D; d++)
+#pragma unroll
+            for (int p = 0; p < ATTN_PREF; p++)
+                r[d][p] = __builtin_nontemporal_load((const u32x4*)(base + (size_t)min(t0 + d * STEP + rr + p * RPP, t1 - 1) * a.kv_dim + col));
+        for (int k = 0; k < nr; k += D) {
+#pragma unroll
+            for (int d = 0; d < D; d++) {
+#pragma unroll
+                for (int p = 0; p < ATTN_PREF; p++) acc ^= r[d][p].x ^ r[d][p].w;
+#pragma unroll
+                for (int p = 0; p < ATTN_PREF; p++)
+                    r[d][p] = __builtin_nontemporal_load((const u32x4*)(base + (size_t)min(t0 + (k + d + D) * STEP + rr + p * RPP, t1 - 1) * a.kv_dim + col));
+            }
+        }
+    }
+    if (acc == 0x12345678u) sink[0] = acc;
 }
 
 int main(int argc, char** argv) {
@@ -95,6 +132,13 @@ int main(int argc, char** argv) {
     };
     printf("kv_len %d (%.1f MB of K+V), slot pitch %d\n", kv_len, 2.0 * kv_len * KVD * 2 / 1e6, PITCH);
     const bool quick = argc > 3;
+    for (int ns : {32, 64}) {
+        const int T = attn_split_len(kv_len, ns, attn_min_t_partials(HD, 1024));
+        run(k_stream<1024, 2>, 1024, ns, 0, "stream  t1024 D2");
+        run(k_stream<1024, 3>, 1024, ns, 0, "stream  t1024 D3");
+        run(k_stream<1024, 4>, 1024, ns, 0, "stream  t1024 D4");
+        run(k_round<1024>, 1024, ns, attn_smem_bytes(HD, QPK, T, ns, 1024), "round   t1024");
+    }
     for (int ns : {32, 64, 128}) {
         if (quick && ns != 32) continue;
         const int T = attn_split_len(kv_len, ns, attn_min_t_partials(HD, 1024));

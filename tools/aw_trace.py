@@ -14,6 +14,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--workload", default="mistral-7b-f16")
     ap.add_argument("--fuse", type=int, default=1, help="XH_OPT_FUSE_ATTN_WO (2: W1/W3 role traced too)")
+    ap.add_argument("--aw-threads", type=int, default=1024, help="AW_THREADS of the library (XALM_HIP_LIB)")
     args = ap.parse_args()
     w = bench.WORKLOADS[args.workload]
     c = bench.make_config(w)
@@ -49,7 +50,8 @@ def main():
     # attention workgroups: stamp 1 = done (0 if it exited as an inactive split: then = start)
     nsplit = max(1, min(256 // nkv, 128, (c.max_seq_len + 255) // 256))  # attn_nsplit (xalm_hip.hip)
     # Wo workgroups (AwShape: 16 waves x 2 rows, one round of <= 4096 waves): ceil(dim / 32)
-    nb_wo = (c.dim + 31) // 32
+    rows_per_wg = 2 * args.aw_threads // 64
+    nb_wo = (c.dim + rows_per_wg - 1) // rows_per_wg
     att = [i for i in used if i < nkv * nsplit]
     wo = [i for i in used if nkv * nsplit <= i < nkv * nsplit + nb_wo]
     mlp = [i for i in used if i >= nkv * nsplit + nb_wo]

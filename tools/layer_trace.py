@@ -63,6 +63,11 @@ def main():
         end = t[:, 2][t[:, 2] != 0]
         stg = t[:, 1][t[:, 1] != 0]
         e = us(end) if end.size else np.array([np.nan])
+        if os.environ.get("XLANDED") and stride == 4:
+            xl = t[:, 3][(t[:, 3] != 0) & (t[:, 3] > t[:, 0].min())]
+            if xl.size:
+                q = np.percentile(us(xl), [10, 50, 90])
+                print(f"{name:8s} x landed p10 {q[0]:7.2f} med {q[1]:7.2f} p90 {q[2]:7.2f}")
         print(f"{name:8s} wgs {t.shape[0]:4d}  start {s0:7.2f}..{s1:7.2f}  staged med {np.median(us(stg)) if stg.size else float('nan'):7.2f}"
               f"  end min {np.min(e):7.2f} med {np.median(e):7.2f} max {np.max(e):7.2f}  span {np.max(e) - s0:6.2f} us")
         spans.append((name, s0, np.max(e)))

@@ -626,6 +626,9 @@ __device__ __forceinline__ void stage_x_finish(const GemvArgs& a, const float4 (
             ss += ((int)threadIdx.x + j * S::THREADS < n4) ? d : 0.f;
         }
         ss = wave_sum(ss);
+#ifdef GEMV_TRACE_X
+        if (a.trace && threadIdx.x == GEMV_TRACE_X * 64) a.trace[4 * blockIdx.x + 3] = __builtin_amdgcn_s_memrealtime();  // x landed (that wave)
+#endif
         if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
         __syncthreads();
         float tot = 0.f;
@@ -633,6 +636,14 @@ __device__ __forceinline__ void stage_x_finish(const GemvArgs& a, const float4 (
         for (int w = 0; w < S::WAVES; w++) tot += red[w];
         scale = 1.0f / sqrtf(tot / (float)a.n + a.eps);
     }
+#ifdef GEMV_TRACE_X
+    if (PRO == PRO_PLAIN && a.trace && threadIdx.x == GEMV_TRACE_X * 64) {
+        float t = 0.f;
+#pragma unroll
+        for (int j = 0; j < S::XN; j++) t += xv[j].x;  // waits for this thread's x loads
+        a.trace[4 * blockIdx.x + 3] = __builtin_amdgcn_s_memrealtime() + (t == 12345.f ? 1 : 0);
+    }
+#endif
 #pragma unroll
     for (int j = 0; j < S::XN; j++) {
         const int i = min((int)threadIdx.x + j * S::THREADS, n4 - 1);
@@ -663,12 +674,17 @@ __device__ __forceinline__ void gemv_body(const GemvArgs& a, const int block, co
     const int lane = threadIdx.x & 63;
     const int wid = threadIdx.x >> 6;
     const int g = block * S::WAVES + wid;
+#ifdef GEMV_TRACE_START
+    if (a.trace && threadIdx.x == GEMV_TRACE_START * 64) a.trace[4 * block + 3] = __builtin_amdgcn_s_memrealtime();
+#endif
     if (a.trace && threadIdx.x == 0) {
         a.trace[4 * block] = __builtin_amdgcn_s_memrealtime();
+#if !defined(GEMV_TRACE_X) && !defined(GEMV_TRACE_START)
         unsigned xcc, hw;
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 3)" : "=s"(xcc));
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
         a.trace[4 * block + 3] = ((unsigned long long)xcc << 32) | hw;  // XCD, HW_ID (CU / SE bits)
+#endif
     }
     if (a.aw_reset && block == 0 && threadIdx.x < AW_RESET_WORDS) a.aw_reset[32 * threadIdx.x] = 0u;
     unsigned long long best = 0;  // EPI_LOGITS: this wave's best candidate (lane 0)
