@@ -7,8 +7,10 @@
 //   o_h = sum_t p_t V[t, g],   g = h / (n_heads / n_kv_heads)
 // One workgroup (16 waves) serves one KV head and a contiguous slot range, so each K/V row is
 // read from HBM once for all q heads of its group (the CPU re-reads it per q head).  K and V
-// rows of ATTN_PREF passes (ATTN_PREF * 1024 / (hd/8) slots: 256 at hd = 128) are requested
-// together at kernel start, so a split of up to 256 slots is one HBM round trip.  The split
+// rows of the first round (ATTN_PREF passes: 256 slots at hd = 128 for the short splits of the
+// fused launch) are requested together at kernel start, so a short split is one HBM round trip;
+// long splits stream rounds of ATTN_PREF_LONG passes with the next round in flight, with
+// non-temporal loads (each row is read once per step).  The split
 // length T is chosen on device from kv_len (grid shape fixed for graph replay): kv_len <= 256
 // needs no merge at all.  With more than one active split, every block stores its partial
 // (o, m, l) write-through and the last block of each KV head to arrive merges them (ticket
@@ -23,7 +25,14 @@ namespace xalm {
 
 constexpr int ATTN_THREADS = 1024;
 constexpr int ATTN_WAVES = ATTN_THREADS / 64;
-constexpr int ATTN_PREF = 4;     // K/V passes held in registers per round
+// K/V passes held in registers per round (two rounds in flight).  Short splits (PARTIALS: the
+// fused launch's chain at short histories) take 4 with default-policy loads: the whole split in
+// the first round trip.  Long splits stream: 2 with non-temporal loads (isolated 32k split
+// 31.0 -> 27.1 us; 4 / 3 passes with nt loads 28.5 / 27.8 us, tools/attn_bench), while the
+// short chain measured slower with either change (4k decode -0.4 % f16, -1.3 % fp8).
+constexpr int ATTN_PREF = 4;
+constexpr int ATTN_PREF_LONG = 2;
+constexpr int ATTN_MIN_ROUNDS = 4;  // the split floor in passes (attn_min_t)
 constexpr int ATTN_MIN_T = 256;  // minimum slots per split
 
 struct AttnArgs {
@@ -48,7 +57,7 @@ __device__ __host__ __forceinline__ int attn_split_len(const int kv_len, const i
     return t < min_t ? min_t : t;
 }
 // one round of K/V rows per block: the split floor of a THREADS-thread block
-__device__ __host__ constexpr int attn_min_t(const int hd, const int threads) { return ATTN_PREF * threads / (hd / 8); }
+__device__ __host__ constexpr int attn_min_t(const int hd, const int threads) { return ATTN_MIN_ROUNDS * threads / (hd / 8); }
 // the fused launch's floor: half a round (each split block pulls half the bytes: a block's
 // K/V fetch is bound by its CU's ~60 GB/s, so more, smaller splits shorten the chain)
 __device__ __host__ constexpr int attn_min_t_partials(const int hd, const int threads) {
@@ -88,6 +97,7 @@ __device__ __forceinline__ void attn_block(const AttnArgs& a, const int g, const
 #define ATTN_STAMP(k) \
     do { if (dbg && threadIdx.x == 0) dbg[k] = __builtin_amdgcn_s_memrealtime(); } while (0)
     constexpr int WAVES = THREADS / 64;
+    constexpr int PREF = PARTIALS ? ATTN_PREF : ATTN_PREF_LONG;
     constexpr int LPR = HD / 8;               // lanes per K/V row (16 B = 8 fp16 each)
     constexpr int RPP = THREADS / LPR;        // rows per pass
     constexpr int NO = QPK * HD;              // outputs of this block
@@ -109,17 +119,19 @@ __device__ __forceinline__ void attn_block(const AttnArgs& a, const int g, const
     const float scale = 1.0f / sqrtf((float)HD);  // src/infer.cpp:338
     const size_t col = (size_t)g * HD + sub * 8;
     auto ld_kv = [&](const uint16_t* base, const int t) {
-        return *(const u32x4*)((const char*)base + ((size_t)t * a.kv_dim + col) * 2);
+        const __attribute__((address_space(1))) u32x4* p =
+            (const __attribute__((address_space(1))) u32x4*)((const char*)base + ((size_t)t * a.kv_dim + col) * 2);
+        return PARTIALS ? *p : __builtin_nontemporal_load(p);
     };
 
     // ---- first round of K and V rows, requested before anything else ----
-    u32x4 kr[ATTN_PREF], vr[ATTN_PREF];
+    u32x4 kr[PREF], vr[PREF];
 #pragma unroll
-    for (int p = 0; p < ATTN_PREF; p++) {
+    for (int p = 0; p < PREF; p++) {
         const int t = t0 + rr + p * RPP;
         if (t < t1) {
-            kr[p] = *(const u32x4*)(a.kc + (size_t)t * a.kv_dim + col);
-            vr[p] = *(const u32x4*)(a.vc + (size_t)t * a.kv_dim + col);
+            kr[p] = ld_kv(a.kc, t);
+            vr[p] = ld_kv(a.vc, t);
         }
     }
     wait();
@@ -146,26 +158,26 @@ __device__ __forceinline__ void attn_block(const AttnArgs& a, const int g, const
             if (sub == 0) sc[h * T + (t - t0)] = p * scale;
         }
     };
-    // rounds of RPP * ATTN_PREF rows, software-pipelined: round r + 1 is requested before round
+    // rounds of RPP * PREF rows, software-pipelined: round r + 1 is requested before round
     // r's dot products.  Two named register sets alternate (unrolled by two): a copy of a
     // register with a load in flight would make the compiler wait for that load, and a load
     // behind a branch would merge into a vmcnt(0); the last round has its own block, so every
     // wait is counted.  (One round in flight per wave left the passes latency-bound at long
     // contexts.)
-    constexpr int STEP = ATTN_PREF * RPP;
-    auto ld_round = [&](u32x4 (&v)[ATTN_PREF], const uint16_t* base_p, const int base) {
+    constexpr int STEP = PREF * RPP;
+    auto ld_round = [&](u32x4 (&v)[PREF], const uint16_t* base_p, const int base) {
 #pragma unroll
-        for (int p = 0; p < ATTN_PREF; p++) v[p] = ld_kv(base_p, min(base + rr + p * RPP, t1 - 1));
+        for (int p = 0; p < PREF; p++) v[p] = ld_kv(base_p, min(base + rr + p * RPP, t1 - 1));
     };
-    auto score_round = [&](const u32x4 (&v)[ATTN_PREF], const int base) {
+    auto score_round = [&](const u32x4 (&v)[PREF], const int base) {
 #pragma unroll
-        for (int p = 0; p < ATTN_PREF; p++) {
+        for (int p = 0; p < PREF; p++) {
             const int t = base + rr + p * RPP;
             if (t < t1) score_row(v[p], t);
         }
     };
     {
-        u32x4 rb[ATTN_PREF];
+        u32x4 rb[PREF];
         int base = t0;
         for (;;) {
             if (base + STEP >= t1) { score_round(kr, base); break; }
@@ -181,7 +193,7 @@ __device__ __forceinline__ void attn_block(const AttnArgs& a, const int g, const
     // V round 1 is requested before the softmax (its loads do not depend on it), so the CU's
     // memory pipe is not empty across the two barriers between the K and V passes (clamped:
     // a split of one round re-reads its last row, unused)
-    u32x4 vn[ATTN_PREF];
+    u32x4 vn[PREF];
     ld_round(vn, a.vc, t0 + STEP);
     __syncthreads();
     ATTN_STAMP(3);
@@ -221,9 +233,9 @@ __device__ __forceinline__ void attn_block(const AttnArgs& a, const int g, const
         }
     };
     {
-        auto pv_round = [&](const u32x4 (&v)[ATTN_PREF], const int base) {
+        auto pv_round = [&](const u32x4 (&v)[PREF], const int base) {
 #pragma unroll
-            for (int p = 0; p < ATTN_PREF; p++) {
+            for (int p = 0; p < PREF; p++) {
                 const int t = base + rr + p * RPP;
                 if (t < t1) pv_row(v[p], t);
             }
