@@ -165,6 +165,11 @@ def host_cpu_info():
     return info
 
 
+def progress(msg):
+    """A progress line on stderr (the JSON result is the only stdout line)."""
+    print(msg, file=sys.stderr, flush=True)
+
+
 def cpu_baseline(w, c, prompt, gpu_logits0, gpu_tokens, n_decode, one_thread_tokens=2):
     """The reference -d cpu path (the oracle: src/infer.cpp restated, OpenMP over matvec rows and
     heads as src/infer.cpp:118 / :438) on the same synthetic weights, timed on this host: hydrate
@@ -187,11 +192,14 @@ def cpu_baseline(w, c, prompt, gpu_logits0, gpu_tokens, n_decode, one_thread_tok
     if w["kv_prefill"]:
         kv_dim = c.n_kv_heads * c.head_dim
         for layer in range(c.n_layers):
+            if layer % 8 == 0:
+                progress(f"cpu baseline: KV history layer {layer} / {c.n_layers}")
             for which in (0, 1):
                 om.set_kv(layer, which, 0, O.synthetic(w["kv_prefill"], kv_dim, L.F16, 5000 + 2 * layer + which,
                                                        0.0, 1.0))
         pos0, hyd = w["kv_prefill"], prompt[:1]
     t_gen = time.time() - t_gen
+    progress(f"cpu baseline: weights ready ({t_gen:.1f} s)")
     threads = O.num_threads()
     ru0 = resource.getrusage(resource.RUSAGE_SELF)
     t0 = time.time()
@@ -205,6 +213,8 @@ def cpu_baseline(w, c, prompt, gpu_logits0, gpu_tokens, n_decode, one_thread_tok
     agree, disagree = 0, []
     t1 = time.time()
     for i in range(n_decode):
+        if i % 8 == 0:
+            progress(f"cpu baseline: decode token {i} / {n_decode}")
         lg = om.logits()
         ref_tok = O.sample_argmax(lg)
         if ref_tok == gpu_tokens[i]:

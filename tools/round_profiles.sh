@@ -4,7 +4,8 @@
 # Each GPU step has its own limit; a crash / abort / timeout ends the run.
 set -u
 cd "$(dirname "$0")/.."
-ROUND=${ROUND:-r02}
+ROUND=${ROUND:-r03}
+PART=${PART:-all}   # a: tests, PMC, kernel trace, fp16 / fp8 benches; b: the other workloads
 OUT=gpurun_out/$ROUND
 mkdir -p "$OUT"
 export TMPDIR=/tmp
@@ -17,6 +18,7 @@ step() {
     echo "== $name rc=$rc"
     if [ $rc -ne 0 ]; then tail -5 "$OUT/$name.log"; exit $rc; fi
 }
+if [ "$PART" != b ]; then
 step smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()"
 step pytest_gpu 900 python3 -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread -rs
 # HBM traffic (MI355X_MICROARCH.md HBM section): FETCH_SIZE and WRITE_SIZE in separate passes
@@ -33,11 +35,14 @@ step kernel_trace 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --o
 cp "$OUT/prof/run_kernel_stats.csv" "$OUT/kernel_stats.csv"
 step bench 600 python3 bench.py
 step bench_f8 600 python3 bench.py --workload mistral-7b-f8
+fi
+if [ "$PART" != a ]; then
 step bench_32k 600 python3 bench.py --workload mistral-7b-f16-32k --steps 64
 step bench_llama 600 python3 bench.py --workload llama3-8b-f16
 # SURVEY 8f-4 block formats (not BASELINE configs; the oracle's per-element block decode makes
 # a CPU sample slow, so none)
 step bench_q8_0 600 python3 bench.py --workload mistral-7b-q8_0 --no-cpu-baseline
 step bench_q4_0 600 python3 bench.py --workload mistral-7b-q4_0 --no-cpu-baseline
-for b in bench bench_f8 bench_32k bench_llama bench_q8_0 bench_q4_0; do tail -1 "$OUT/$b.log" > "$OUT/$b.json"; done
+fi
+for b in bench bench_f8 bench_32k bench_llama bench_q8_0 bench_q4_0; do [ -f "$OUT/$b.log" ] && tail -1 "$OUT/$b.log" > "$OUT/$b.json"; done
 echo "== done"
