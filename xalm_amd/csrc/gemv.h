@@ -95,7 +95,16 @@ __device__ __forceinline__ float act_fn(const int act, const float x) {
     return 0.5f * x * (1.0f + tanhf(0.797885f * (x + 0.044715f * x * x * x)));
 }
 
-// One rope rotation of the adjacent pair (v0, v1) at element index i (src/infer.cpp:308-321).
+// One rope rotation of the adjacent pair (v0, v1) at frequency freq (src/infer.cpp:308-321).
+__device__ __forceinline__ void rope_pair_f(float& v0, float& v1, const float freq, const int pos) {
+    const float val = (float)pos * freq;
+    const float fcr = cosf(val);
+    const float fci = sinf(val);
+    const float a = v0, b = v1;
+    v0 = a * fcr - b * fci;
+    v1 = a * fci + b * fcr;
+}
+// ... at element index i (frequency from the table)
 __device__ __forceinline__ void rope_pair(float& v0, float& v1, const int i, const int head_dim, const int pos,
                                           const float* freq_tab) {
     const int j_head = i % head_dim;
@@ -205,9 +214,20 @@ __device__ __forceinline__ void epi_st(float* p, const float v) {
     if (SC1) st_sc1_f(p, v);
     else *p = v;
 }
+// QKV epilogue inputs requested ahead of the group's weights (gemv_rows_pipe): the step's
+// position, ring slot and the rope frequency of each row pair, so the epilogue at the group's
+// end does not start two dependent loads (StepParams, then the frequency table)
+template <int ROWS>
+struct QkvPre {
+    int pos, kv_pos;
+    float freq[ROWS / 2 > 0 ? ROWS / 2 : 1];
+};
+// res: EPI_RESID's residual rows, requested with the group's first weights (not from the
+// epilogue, where the load would be a dependent round trip at the group's end)
 template <int EPI, int ROWS, bool SC1 = false>
 __device__ __forceinline__ void gemv_epilogue(const GemvArgs& a, const int row0, const float* acc,
-                                              unsigned long long* best = nullptr) {
+                                              unsigned long long* best = nullptr,
+                                              const QkvPre<ROWS>* pre = nullptr, const float* res = nullptr) {
     if (EPI == EPI_LOGITS) {
 #pragma unroll
         for (int r = 0; r < ROWS; r++)
@@ -226,25 +246,30 @@ __device__ __forceinline__ void gemv_epilogue(const GemvArgs& a, const int row0,
     } else if (EPI == EPI_RESID) {
 #pragma unroll
         for (int r = 0; r < ROWS; r++)
-            if (row0 + r < a.rows) epi_st<SC1>(a.out + row0 + r, (SC1 ? ld_sc1_f(a.out + row0 + r) : a.out[row0 + r]) + acc[r]);
+            if (row0 + r < a.rows)
+                epi_st<SC1>(a.out + row0 + r, (res ? res[r] : SC1 ? ld_sc1_f(a.out + row0 + r) : a.out[row0 + r]) + acc[r]);
     } else if (EPI == EPI_GLU) {
 #pragma unroll
         for (int p = 0; p < ROWS; p += 2) epi_st<SC1>(a.out + ((row0 + p) >> 1), act_fn(a.act, acc[p]) * acc[p + 1]);
     } else {  // EPI_QKV
-        const int pos = a.sp->pos;
-        const int kv_pos = a.sp->kv_pos;
+        const int pos = pre ? pre->pos : a.sp->pos;
+        const int kv_pos = pre ? pre->kv_pos : a.sp->kv_pos;
 #pragma unroll
         for (int p = 0; p < ROWS; p += 2) {
             const int row = row0 + p;
             float v0 = clipf(acc[p], a.qkv_clip), v1 = clipf(acc[p + 1], a.qkv_clip);
             if (row < a.q_dim) {
-                rope_pair(v0, v1, row, a.head_dim, pos, a.rope_freq);
+                if (pre) rope_pair_f(v0, v1, pre->freq[p >> 1], pos);
+                else rope_pair(v0, v1, row, a.head_dim, pos, a.rope_freq);
                 epi_st<SC1>(a.q + row, v0);
                 epi_st<SC1>(a.q + row + 1, v1);
             } else {
                 const bool isk = row < a.q_dim + a.kv_dim;
                 const int kr = isk ? row - a.q_dim : row - a.q_dim - a.kv_dim;
-                if (isk) rope_pair(v0, v1, kr, a.head_dim, pos, a.rope_freq);
+                if (isk) {
+                    if (pre) rope_pair_f(v0, v1, pre->freq[p >> 1], pos);  // q_dim % head_dim == 0
+                    else rope_pair(v0, v1, kr, a.head_dim, pos, a.rope_freq);
+                }
                 uint16_t* dst = (isk ? a.kcache : a.vcache) + (size_t)kv_pos * a.kv_dim + kr;
                 // the pair as one 4-byte store (kr is even)
                 const uint32_t pk = (uint32_t)f32_to_f16_bits(v0) | ((uint32_t)f32_to_f16_bits(v1) << 16);
@@ -473,6 +498,12 @@ __device__ __forceinline__ void gemv_group(const GemvArgs& a, const int g, const
     const int n_it = (n + 64 * E - 1) / (64 * E);
     size_t rstride;
     const char* wrow = gemv_row_ptr<ROWS>(a, g, lane, rstride);
+    constexpr bool RES = EPI == EPI_RESID && !SC1;
+    float res[ROWS];
+    if constexpr (RES) {
+#pragma unroll
+        for (int r = 0; r < ROWS; r++) res[r] = a.out[min(g * ROWS + r, a.rows - 1)];
+    }
     if constexpr (WScale<DT>::BLOCK > 0) {
         const size_t qb = gq_qbytes(DT, (size_t)n);
         for (; it + U <= n_full; it += U) gemv_chunk_gq<DT, ROWS, U, S::NT>(wrow, rstride, qb, xs4, it, lane, acc);
@@ -489,7 +520,7 @@ __device__ __forceinline__ void gemv_group(const GemvArgs& a, const int g, const
     }
 #pragma unroll
     for (int r = 0; r < ROWS; r++) acc[r] = wave_sum(acc[r]);
-    if (lane == 0) gemv_epilogue<EPI, ROWS, SC1>(a, g * ROWS, acc, best);
+    if (lane == 0) gemv_epilogue<EPI, ROWS, SC1>(a, g * ROWS, acc, best, nullptr, RES ? res : nullptr);
 }
 
 // Groups g, g + total_waves, ... of this wave against the staged x image.  FIRST: the first
@@ -538,18 +569,40 @@ __device__ __forceinline__ void gemv_rows_pipe(const GemvArgs& a, const int g0, 
     const size_t qb = GQ ? gq_qbytes(DT, (size_t)a.n) : 0;
     // step k of this wave: group g0 + (k / steps) * total_waves, chunks from (k % steps) * U
     const int total = ((n_groups - g0 + total_waves - 1) / total_waves) * steps;
-    auto load = [&](u32x4 (&w)[U][ROWS], float (&d)[U][ROWS], const int k) {
+    // QKV: requested with the weights, ahead of the epilogue that uses them.  One-byte weights
+    // only: fp8 decode 596 -> 603 tok/s, while the 2-byte qkv launch measured 0.5 % slower with it
+    // (same-box A/B, two pairs each)
+    constexpr bool QKV = EPI == EPI_QKV && E >= 16;
+    QkvPre<ROWS> qp{};
+    if constexpr (QKV) {
+        qp.pos = a.sp->pos;
+        qp.kv_pos = a.sp->kv_pos;
+    }
+    // QKV: the rope frequency of each row pair of the step's group; RESID: its residual rows
+    constexpr bool RES = EPI == EPI_RESID && !SC1;
+    float fa[ROWS], fb[ROWS];
+    auto load = [&](u32x4 (&w)[U][ROWS], float (&d)[U][ROWS], float (&f)[ROWS], const int k) {
         const int q = k / steps;
         size_t rs;
         const char* wrow = gemv_row_ptr<ROWS>(a, g0 + q * total_waves, lane, rs);
         gemv_load<ROWS, U, S::NT>(w, wrow, rs, (k - q * steps) * U);
         if constexpr (GQ) gq_load_scales<DT, ROWS, U>(d, wrow, rs, qb, (k - q * steps) * U, lane);
+        if constexpr (QKV) {
+            const int row0 = min((g0 + q * total_waves) * ROWS, a.rows - ROWS);
+#pragma unroll
+            for (int p = 0; p < ROWS; p += 2) f[p >> 1] = a.rope_freq[((row0 + p) % a.head_dim) >> 1];
+        }
+        if constexpr (RES) {
+            const int row0 = (g0 + q * total_waves) * ROWS;
+#pragma unroll
+            for (int r = 0; r < ROWS; r++) f[r] = a.out[min(row0 + r, a.rows - 1)];
+        }
     };
     float acc[ROWS];
 #pragma unroll
     for (int r = 0; r < ROWS; r++) acc[r] = 0.f;
     // multiply step k's chunks; after a group's last step, its reduction and epilogue
-    auto step = [&](const u32x4 (&w)[U][ROWS], const float (&d)[U][ROWS], const int k) {
+    auto step = [&](const u32x4 (&w)[U][ROWS], const float (&d)[U][ROWS], const float (&f)[ROWS], const int k) {
         const int q = k / steps;
         const int it = (k - q * steps) * U;
         if constexpr (GQ) gq_compute<DT, ROWS, U>(w, d, xs4, it, lane, acc);
@@ -557,7 +610,13 @@ __device__ __forceinline__ void gemv_rows_pipe(const GemvArgs& a, const int g0, 
         if (it + U == steps * U) {
 #pragma unroll
             for (int r = 0; r < ROWS; r++) acc[r] = wave_sum(acc[r]);
-            if (lane == 0) gemv_epilogue<EPI, ROWS, SC1>(a, (g0 + q * total_waves) * ROWS, acc, best);
+            if constexpr (QKV) {
+#pragma unroll
+                for (int p = 0; p < ROWS; p += 2) qp.freq[p >> 1] = f[p >> 1];
+            }
+            if (lane == 0)
+                gemv_epilogue<EPI, ROWS, SC1>(a, (g0 + q * total_waves) * ROWS, acc, best, QKV ? &qp : nullptr,
+                                              RES ? f : nullptr);
 #pragma unroll
             for (int r = 0; r < ROWS; r++) acc[r] = 0.f;
         }
@@ -572,23 +631,32 @@ __device__ __forceinline__ void gemv_rows_pipe(const GemvArgs& a, const int g0, 
                 wa[u][r] = pre[u][r];
                 if constexpr (GQ) da[u][r] = pre_d[u][r];
             }
+        if constexpr (QKV) {
+            const int row0 = min(g0 * ROWS, a.rows - ROWS);
+#pragma unroll
+            for (int p = 0; p < ROWS; p += 2) fa[p >> 1] = a.rope_freq[((row0 + p) % a.head_dim) >> 1];
+        }
+        if constexpr (RES) {
+#pragma unroll
+            for (int r = 0; r < ROWS; r++) fa[r] = a.out[min(g0 * ROWS + r, a.rows - 1)];
+        }
     } else {
-        load(wa, da, 0);
+        load(wa, da, fa, 0);
     }
     // the loads stay outside any branch, so the compiler's waits count only the older set
     int k = 0;
     for (; k + 2 < total; k += 2) {
-        load(wb, db, k + 1);
-        step(wa, da, k);
-        load(wa, da, k + 2);
-        step(wb, db, k + 1);
+        load(wb, db, fb, k + 1);
+        step(wa, da, fa, k);
+        load(wa, da, fa, k + 2);
+        step(wb, db, fb, k + 1);
     }
     if (k + 1 < total) {
-        load(wb, db, k + 1);
-        step(wa, da, k);
-        step(wb, db, k + 1);
+        load(wb, db, fb, k + 1);
+        step(wa, da, fa, k);
+        step(wb, db, fb, k + 1);
     } else {
-        step(wa, da, k);
+        step(wa, da, fa, k);
     }
 }
 
