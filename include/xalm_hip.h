@@ -181,22 +181,27 @@ int xh_set_graphs(xh_ctx* ctx, int enable);
 /* Launch-structure variants.  XH_OPT_FUSE_ATTN_WO (default 1): 1 = attention and Wo (+ residual)
  * in one launch with an in-launch hand-off (attn_wo.h); 0 = two launches.  Same math. */
 /* XH_OPT_PREFILL (default 1): xh_prefill / xh_perplexity process the prompt in passes, each
- * weight matrix streamed once per pass into a GEMM (prefill.h).  1 = f16 and fp8 weights on
- * hipBLASLt in passes of 512 tokens (fp8 matrices through their exact f16 image), activations
- * as exact f16 hi + lo pairs under a power-of-two row scale (≈22-bit mantissa, f32
- * accumulation); other dtypes on the f32-input MFMA kernel (activations exactly as the reference),
- * passes of 64 tokens when any layer's GEMM is off hipBLASLt; 2 = the split-f16 MFMA kernel
- * wherever the weights convert exactly to f16 (f16, fp8); 3 = f32-input MFMA only; 0 = one
- * forward per token (the reference's loop, src/main.cpp:94-100).  Same math per token up to
- * f32 rounding. */
+ * weight matrix streamed once per pass into a GEMM.  1 = f16 and fp8 weights on the LDS-tiled MFMA
+ * GEMM (gemm16.h) in passes of up to 1024 tokens (fp8 matrices through their exact f16 image),
+ * activations as exact f16 hi + lo pairs under a power-of-two row scale (|x - (hi + lo) / s| <=
+ * 2^-22 |x|, a 22-bit mantissa where the reference's f32 has 24), products exact, f32
+ * accumulation in an order fixed by the tiling (the same bits on every run); other weight dtypes
+ * on the f32-input MFMA kernel (activations exactly as the reference) in passes of 64 tokens;
+ * 2 = the split-f16 register-streaming MFMA kernel wherever the weights convert exactly to f16
+ * (f16, fp8), passes of 64 tokens; 3 = f32-input MFMA only; 4 = as 1 with vendor hipBLASLt in place
+ * of gemm16.h (passes of 512 tokens, the heuristic's first algorithm: deterministic per library
+ * build); 0 = one forward per token (the reference's loop, src/main.cpp:94-100).  Same math per
+ * token up to f32 rounding. */
 /* XH_OPT_PREFILL_GLU_SPLIT (default 1): where the W2 GEMM takes split-f16 input, the GLU
- * epilogue of the W1/W3 GEMM writes those f16 hi/lo fragments directly (one launch); 0 = GLU to
+ * epilogue of the W1/W3 GEMM writes those f16 hi/lo halves directly (one launch); 0 = GLU to
  * f32 first, then split in the W2 GEMM's input pass (two launches).  Bit-identical results; a
  * debug knob so tests cover both routes. */
 /* XH_OPT_PREFILL_ATTN (default 1): the batched path's causal attention on MFMA tiles (32 query
  * rows x 32-slot K/V tiles per wave, running max/sum, q and p as exact f16 hi + lo pairs);
- * 0 = one workgroup per token and KV head, split-KV f32 FMA (the decode attention's blocks). */
-enum xh_option { XH_OPT_FUSE_ATTN_WO = 1, XH_OPT_PREFILL = 2, XH_OPT_PREFILL_GLU_SPLIT = 3, XH_OPT_PREFILL_ATTN = 4 };
+ * 0 = one workgroup per token and KV head, split-KV f32 FMA (the decode attention's blocks).
+ * Option id 4 (XH_OPT_COL_KV_MAX, removed in round 3 with the column-form attention) is no
+ * longer accepted: xh_set_option / xh_get_option return XH_E_INVALID for it. */
+enum xh_option { XH_OPT_FUSE_ATTN_WO = 1, XH_OPT_PREFILL = 2, XH_OPT_PREFILL_GLU_SPLIT = 3, XH_OPT_PREFILL_ATTN = 5 };
 int xh_set_option(xh_ctx* ctx, int option, int value);
 int xh_get_option(const xh_ctx* ctx, int option, int* value);
 
@@ -210,6 +215,14 @@ int xh_op_rope(float* vec, int d, int head_dim, int pos, float theta, int rotary
 /* mha_cuda (src/model.h:308-313): xout[n_heads*head_dim]; kb/vb fp16 [max_seq_len][n_kv_heads*head_dim]. */
 int xh_op_mha(float* xout, const uint16_t* kb, const uint16_t* vb, const float* q, int head_dim,
               int kv_len, int max_seq_len, int n_heads, int n_kv_heads);
+
+/* The prompt-pass GEMM of XH_OPT_PREFILL 1 (gemm16.h): y[t][r] = sum_k w[r][k] * (xh[t][k] + xl[t][k])
+ * with f16 w [rows][K], f16 xh / xl [n][K] and f32 y [n][rows] (the K slices' partials summed in
+ * slice order, as the prompt path's epilogue).  K % 64 == 0; ks = K slices (0: the prompt path's
+ * choice for this shape).  No reference counterpart: the matmul of src/infer.cpp:104-135 over n
+ * tokens at once. */
+int xh_op_prompt_gemm(float* y, const uint16_t* w, const uint16_t* xh, const uint16_t* xl, int rows, int K, int n,
+                      int ks);
 
 /* ---- timing hooks used by bench.py (HIP events on the context's own stream) -------- */
 /* Average device time (microseconds) of one launch of kernel `which` (0 = the fused

@@ -43,6 +43,7 @@ def _load():
             "xo_num_threads": (_I, []), "xo_set_threads": (None, [_I]),
             "xo_set_matmul_order": (None, [_I]), "xo_matmul_order": (_I, []),
             "xo_fill_synthetic": (None, [_P, _SZ, _SZ, _I, ctypes.c_uint64, ctypes.c_float, ctypes.c_float]),
+            "xo_set_precision": (None, [_P, _I]), "xo_precision": (_I, [_P]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -86,6 +87,13 @@ class OracleModel:
         rc = _load().xo_set_tensor(self.m, kind, layer, dtype, _p(arr))
         if rc:
             raise ValueError(f"xo_set_tensor rc={rc}")
+
+    def set_precision(self, p):
+        """1: this model's forward evaluated in double (every product, sum, norm, softmax,
+        activation and residual), the fp16 K/V cache and the reference's float rope angles kept,
+        logits rounded to float: the algorithm's value independent of f32 rounding order.
+        0 (default): the reference's f32 arithmetic."""
+        _load().xo_set_precision(self.m, int(p))
 
     def forward(self, token, pos, mode=1):
         rc = _load().xo_forward(self.m, int(token), int(pos), int(mode))

@@ -203,6 +203,29 @@ void xo_matmul(float* xout, const float* x, const void* w, const int dtype, cons
         }
         return;
     }
+#ifdef XO_SIMD
+    if (dtype == XH_F16) {
+        /* sequential order: the same left-to-right product + sum as the generic loop below
+         * (separate multiply and add), with the f16 -> f32 conversions done 8 at a time */
+        const uint16_t* W = (const uint16_t*)w;
+#pragma omp parallel for schedule(static)
+        for (i = 0; i < d; i++) {
+            const uint16_t* row = W + (size_t)i * n;
+            float val = 0.0f, f[8];
+            int j = 0;
+            for (; j + 8 <= n; j += 8) {
+                _mm256_storeu_ps(f, _mm256_cvtph_ps(_mm_loadu_si128((const __m128i*)(row + j))));
+                for (int e = 0; e < 8; e++) {
+                    const float p = f[e] * x[j + e];
+                    val += p;
+                }
+            }
+            for (; j < n; j++) val += xo_f16_to_f32(row[j]) * x[j];
+            xout[i] = val;
+        }
+        return;
+    }
+#endif
 #define XO_MATMUL_LOOP(T, DEC)                                              \
     {                                                                       \
         const T* W = (const T*)w;                                           \
@@ -356,6 +379,10 @@ struct xo_model {
     xo_block* blocks;
     /* InferenceState, src/model.h:97-108 */
     float *x, *xb, *xb2, *hb, *hb2, *q, *k, *v, *att, *logits;
+    /* the same state in double for the fp64 evaluation (xo_set_precision(m, 1)), allocated on
+     * first use */
+    double *dx, *dxb, *dxb2, *dhb, *dhb2, *dq, *dk, *dv, *datt;
+    int prec64;
 };
 
 static void* xcalloc(size_t n, size_t sz) { return calloc(n ? n : 1, sz); }
@@ -397,6 +424,8 @@ void xo_destroy(xo_model* m) {
     free(m->blocks);
     free(m->x); free(m->xb); free(m->xb2); free(m->hb); free(m->hb2);
     free(m->q); free(m->k); free(m->v); free(m->att); free(m->logits);
+    free(m->dx); free(m->dxb); free(m->dxb2); free(m->dhb); free(m->dhb2);
+    free(m->dq); free(m->dk); free(m->dv); free(m->datt);
     free(m);
 }
 
@@ -512,6 +541,194 @@ static void block_cpu(xo_model* m, const xo_block* b, const int pos, const int k
     for (int i = 0; i < c->dim; ++i) m->x[i] += m->xb2[i];
 }
 
+/* ------------------------------------------------------------------------------------ */
+/* fp64 evaluation of the same algorithm (xo_set_precision(m, 1))                           */
+/* ------------------------------------------------------------------------------------ */
+/* Every product, sum, norm, softmax, activation and residual of src/infer.cpp:224-638 in
+ * double, so the result is the reference algorithm's value up to ~1e-16 relative: a
+ * precision-independent yardstick for "how far is an f32 evaluation from the algorithm's
+ * exact value".  Kept exactly as the reference defines them, because they are part of the
+ * algorithm rather than of its arithmetic precision: the weights (decoded to their exact
+ * values), the fp16 K/V cache (every stored K/V element rounded to fp16, src/infer.cpp:410-414,
+ * and the sink re-rotation's fp16 round trip :421-431), the rope angle table (the float
+ * expressions `1.0f / powf(theta, j / rot)` and `pos * freq` of :310-314; cos / sin of that angle
+ * in double) and the FLT_MIN start of the sampler.  Logits are returned rounded to float. */
+void xo_set_precision(xo_model* m, int p) { m->prec64 = p != 0; }
+int xo_precision(const xo_model* m) { return m->prec64; }
+
+static double* dcalloc(size_t n) { return (double*)xcalloc(n, sizeof(double)); }
+
+static int alloc64(xo_model* m) {
+    if (m->dx) return 0;
+    const xh_config* c = &m->c;
+    const size_t q_dim = (size_t)c->n_heads * c->head_dim, kv_dim = (size_t)c->n_kv_heads * c->head_dim;
+    const size_t xb2n = q_dim > (size_t)c->dim ? q_dim : (size_t)c->dim;
+    const size_t hbn = (size_t)c->hidden_dim > (size_t)c->dim ? (size_t)c->hidden_dim : (size_t)c->dim;
+    m->dx = dcalloc(c->dim); m->dxb = dcalloc(c->dim); m->dxb2 = dcalloc(xb2n);
+    m->dhb = dcalloc(hbn); m->dhb2 = dcalloc(c->hidden_dim);
+    m->dq = dcalloc(q_dim); m->dk = dcalloc(kv_dim); m->dv = dcalloc(kv_dim);
+    m->datt = dcalloc((size_t)c->n_heads * c->max_seq_len);
+    return m->dx && m->dxb && m->dxb2 && m->dhb && m->dhb2 && m->dq && m->dk && m->dv && m->datt ? 0 : XH_E_INVALID;
+}
+
+/* matmul (src/infer.cpp:104-135) with double products and a double accumulator */
+static void matmul64(double* xout, const double* x, const void* w, const int dtype, const int n, const int d) {
+    int i;
+    if (dtype == XH_F16) {
+        const uint16_t* W = (const uint16_t*)w;
+#pragma omp parallel for schedule(static)
+        for (i = 0; i < d; i++) {
+            const uint16_t* row = W + (size_t)i * n;
+            int j = 0;
+            double val = 0.0;
+#ifdef XO_SIMD
+            __m256d a0 = _mm256_setzero_pd(), a1 = _mm256_setzero_pd();
+            for (; j + 8 <= n; j += 8) {
+                const __m256 f = _mm256_cvtph_ps(_mm_loadu_si128((const __m128i*)(row + j)));
+                a0 = _mm256_fmadd_pd(_mm256_cvtps_pd(_mm256_castps256_ps128(f)), _mm256_loadu_pd(x + j), a0);
+                a1 = _mm256_fmadd_pd(_mm256_cvtps_pd(_mm256_extractf128_ps(f, 1)), _mm256_loadu_pd(x + j + 4), a1);
+            }
+            double t[4];
+            _mm256_storeu_pd(t, _mm256_add_pd(a0, a1));
+            val = (t[0] + t[1]) + (t[2] + t[3]);
+#endif
+            for (; j < n; j++) val += (double)xo_f16_to_f32(row[j]) * x[j];
+            xout[i] = val;
+        }
+        return;
+    }
+#pragma omp parallel for schedule(static)
+    for (i = 0; i < d; i++) {
+        double val = 0.0;
+        for (int j = 0; j < n; j++) val += (double)xo_decode_row(dtype, w, (size_t)i, (size_t)n, (size_t)j) * x[j];
+        xout[i] = val;
+    }
+}
+
+/* rmsnorm, src/infer.cpp:224-236 */
+static void rmsnorm64(double* o, const double* x, const void* w, const int dtype, const int size, const float eps) {
+    double ss = 0.0;
+    for (int i = 0; i < size; ++i) ss += x[i] * x[i];
+    const double scale = 1.0 / sqrt(ss / (double)size + (double)eps);
+    for (int i = 0; i < size; ++i) {
+        const double wi = dtype == XH_BF16 ? bf16_to_f32(((const uint16_t*)w)[i]) : ((const float*)w)[i];
+        o[i] = x[i] * scale * wi;
+    }
+}
+
+/* rope, src/infer.cpp:305-322: the reference's float angle, rotated in double */
+static void rope64(double* vec, const int d, const int head_dim, const int pos, const float theta, const int rotary_dim) {
+    for (int i = 0; i < d; i += 2) {
+        const int j_head = i % head_dim;
+        const float freq = j_head >= rotary_dim ? 0.f : 1.0f / powf(theta, (float)j_head / (float)rotary_dim);
+        const float val = (float)pos * freq;
+        const double fcr = cos((double)val), fci = sin((double)val);
+        const double v0 = vec[i], v1 = vec[i + 1];
+        vec[i] = v0 * fcr - v1 * fci;
+        vec[i + 1] = v0 * fci + v1 * fcr;
+    }
+}
+
+/* attn + softmax, src/infer.cpp:280-297, 325-359 */
+static void attn64(double* xout, double* atth, const double* qh, const uint16_t* kh, const uint16_t* vh,
+                   const int head_dim, const int n_kv_heads, const int kv_len) {
+    const int kv_stride = n_kv_heads * head_dim;
+    const double inv_sqrt = 1.0 / sqrt((double)head_dim);
+    double mx = -DBL_MAX;
+    for (int t = 0; t < kv_len; ++t) {
+        double score = 0.0;
+        for (int i = 0; i < head_dim; ++i) score += qh[i] * (double)xo_f16_to_f32(kh[(size_t)t * kv_stride + i]);
+        atth[t] = score * inv_sqrt;
+        if (atth[t] > mx) mx = atth[t];
+    }
+    double sum = 0.0;
+    for (int t = 0; t < kv_len; ++t) {
+        atth[t] = exp(atth[t] - mx);
+        sum += atth[t];
+    }
+    for (int t = 0; t < kv_len; ++t) atth[t] /= sum;
+    for (int i = 0; i < head_dim; ++i) {
+        double vi = 0.0;
+        for (int t = 0; t < kv_len; ++t) vi += atth[t] * (double)xo_f16_to_f32(vh[(size_t)t * kv_stride + i]);
+        xout[i] = vi;
+    }
+}
+
+static inline double clip64(const double x, const double v) { return x < -v ? -v : (x > v ? v : x); }
+/* the fp16 cache store of a double: rounded once to float, then to fp16 as the reference */
+static inline uint16_t f16_of(const double v) { return xo_f32_to_f16((float)v); }
+
+/* Block::_block_cpu, src/infer.cpp:365-496, in double */
+static void block64(xo_model* m, const xo_block* b, const int pos, const int kv_sink, const int kv_pos,
+                    const int kv_len) {
+    const xh_config* c = &m->c;
+    const xo_tensor* t = b->t;
+    const int q_dim = c->n_heads * c->head_dim, kv_dim = c->n_kv_heads * c->head_dim;
+    const double vclip = (double)c->qkv_clip;
+    rmsnorm64(m->dxb, m->dx, t[XH_ATTN_NORM].data, t[XH_ATTN_NORM].dtype, c->dim, c->norm_eps);
+    matmul64(m->dq, m->dxb, t[XH_WQ].data, t[XH_WQ].dtype, c->dim, q_dim);
+    matmul64(m->dk, m->dxb, t[XH_WK].data, t[XH_WK].dtype, c->dim, kv_dim);
+    matmul64(m->dv, m->dxb, t[XH_WV].data, t[XH_WV].dtype, c->dim, kv_dim);
+    for (int i = 0; i < q_dim; ++i) m->dq[i] = clip64(m->dq[i], vclip);
+    for (int i = 0; i < kv_dim; ++i) {
+        m->dk[i] = clip64(m->dk[i], vclip);
+        m->dv[i] = clip64(m->dv[i], vclip);
+    }
+    uint16_t* kb = b->key_cache;
+    uint16_t* vb = b->value_cache;
+    rope64(m->dq, q_dim, c->head_dim, pos, c->rope_theta, c->rotary_dim);
+    rope64(m->dk, kv_dim, c->head_dim, pos, c->rope_theta, c->rotary_dim);
+    for (int i = 0; i < kv_dim; ++i) {
+        kb[(size_t)kv_pos * kv_dim + i] = f16_of(m->dk[i]);
+        vb[(size_t)kv_pos * kv_dim + i] = f16_of(m->dv[i]);
+    }
+    for (int r = 0; r < kv_sink; r++) {
+        for (int i = 0; i < kv_dim; ++i) m->dk[i] = xo_f16_to_f32(kb[(size_t)r * kv_dim + i]);
+        rope64(m->dk, kv_dim, c->head_dim, 1, c->rope_theta, c->rotary_dim);
+        for (int i = 0; i < kv_dim; i++) kb[(size_t)r * kv_dim + i] = f16_of(m->dk[i]);
+    }
+    const int qpk = c->n_heads / c->n_kv_heads;
+    int h;
+#pragma omp parallel for schedule(static)
+    for (h = 0; h < c->n_heads; h++) {
+        const int kvo = (h / qpk) * c->head_dim;
+        attn64(m->dxb2 + (size_t)c->head_dim * h, m->datt + (size_t)c->max_seq_len * h, m->dq + (size_t)c->head_dim * h,
+               kb + kvo, vb + kvo, c->head_dim, c->n_kv_heads, kv_len);
+    }
+    matmul64(m->dhb, m->dxb2, t[XH_WO].data, t[XH_WO].dtype, q_dim, c->dim);
+    for (int i = 0; i < c->dim; ++i) m->dx[i] += m->dhb[i];
+    rmsnorm64(m->dxb, m->dx, t[XH_FFN_NORM].data, t[XH_FFN_NORM].dtype, c->dim, c->norm_eps);
+    matmul64(m->dhb, m->dxb, t[XH_W1].data, t[XH_W1].dtype, c->dim, c->hidden_dim);
+    matmul64(m->dhb2, m->dxb, t[XH_W3].data, t[XH_W3].dtype, c->dim, c->hidden_dim);
+    for (int i = 0; i < c->hidden_dim; ++i) {
+        const double g = m->dhb[i];
+        const double a = c->act == XH_ACT_GELU ? 0.5 * g * (1.0 + tanh(0.797885 * (g + 0.044715 * g * g * g)))
+                                               : g / (1.0 + exp(-g));
+        m->dhb[i] = a * m->dhb2[i];
+    }
+    matmul64(m->dxb2, m->dhb, t[XH_W2].data, t[XH_W2].dtype, c->hidden_dim, c->dim);
+    for (int i = 0; i < c->dim; ++i) m->dx[i] += m->dxb2[i];
+}
+
+static int forward64(xo_model* m, const int token, const int pos, const int mode, const int kv_sink, const int kv_pos,
+                     const int kv_len) {
+    const xh_config* c = &m->c;
+    if (alloc64(m)) return XH_E_INVALID;
+    for (int i = 0; i < c->dim; ++i) m->dx[i] = xo_decode_row(m->embed.dtype, m->embed.data, (size_t)token, c->dim, i);
+    for (int l = 0; l < c->n_layers; l++) block64(m, &m->blocks[l], pos, kv_sink, kv_pos, kv_len);
+    if (mode == XH_HYDRATE_KV_CACHE) return 0;
+    rmsnorm64(m->dx, m->dx, m->final_norm.data, m->final_norm.dtype, c->dim, c->norm_eps);
+    /* lm_head into dhb-sized scratch is too small for the vocabulary: rows in chunks */
+    double out[256];
+    for (int r0 = 0; r0 < c->vocab_size; r0 += 256) {
+        const int rows = c->vocab_size - r0 < 256 ? c->vocab_size - r0 : 256;
+        const size_t rb = row_bytes(m->wcls.dtype, c->dim);
+        matmul64(out, m->dx, (const char*)m->wcls.data + (size_t)r0 * rb, m->wcls.dtype, c->dim, rows);
+        for (int i = 0; i < rows; i++) m->logits[r0 + i] = (float)out[i];
+    }
+    return 0;
+}
+
 /* Model::_forward_cpu, src/infer.cpp:604-638 */
 int xo_forward(xo_model* m, const int token, const int pos, const int mode) {
     const xh_config* c = &m->c;
@@ -520,11 +737,12 @@ int xo_forward(xo_model* m, const int token, const int pos, const int mode) {
     for (int l = 0; l < c->n_layers; l++)
         for (int k = XH_ATTN_NORM; k <= XH_W3; k++)
             if (!m->blocks[l].t[k].data) return XH_E_STATE;
-    copy_embedding(m, token);
     /* ring / sink bookkeeping :611-613 */
     const int kv_sink = pos >= c->max_seq_len ? KV_SINKS : 0;
     const int kv_pos = kv_sink + (pos - kv_sink) % (c->max_seq_len - kv_sink);
     const int kv_len = pos >= c->max_seq_len ? c->max_seq_len : pos + 1;
+    if (m->prec64) return forward64(m, token, pos, mode, kv_sink, kv_pos, kv_len);
+    copy_embedding(m, token);
     for (int l = 0; l < c->n_layers; l++) block_cpu(m, &m->blocks[l], pos, kv_sink, kv_pos, kv_len);
     if (mode == XH_HYDRATE_KV_CACHE) return 0; /* :620-623 */
     xo_rmsnorm(m->x, m->x, m->final_norm.data, m->final_norm.dtype, c->dim, c->norm_eps); /* :626-634 */

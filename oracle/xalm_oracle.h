@@ -31,6 +31,11 @@ int xo_set_tensor(xo_model* m, int kind, int layer, int dtype, const void* data)
 /* Model::_forward_cpu (src/infer.cpp:604-638). Returns 0 on success. */
 int xo_forward(xo_model* m, int token, int pos, int mode);
 const float* xo_logits(const xo_model* m);
+/* 1: evaluate this model's forward in double (products, sums, norms, softmax, activations,
+ * residuals) with the fp16 K/V cache and the reference's float rope angles kept; logits
+ * rounded to float.  0 (default): the reference's f32 arithmetic. */
+void xo_set_precision(xo_model* m, int p);
+int xo_precision(const xo_model* m);
 uint16_t* xo_key_cache(xo_model* m, int layer);   /* fp16 bits [max_seq_len][kv_dim] */
 uint16_t* xo_value_cache(xo_model* m, int layer);
 size_t xo_active_bytes(const xo_model* m, size_t pos);

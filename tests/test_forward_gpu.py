@@ -138,15 +138,16 @@ def test_prefill_matches_oracle(name, context, engine):
         assert np.abs(a - b).max() <= 2e-3 * max(1.0, np.abs(b).max())
 
 
-@pytest.mark.parametrize("mode", [1, 2, 3])
+@pytest.mark.parametrize("mode", [1, 2, 3, 4])
 @pytest.mark.parametrize("name", FIXTURES)
 @pytest.mark.parametrize("n", [1, 37, 64, 150])
 def test_batched_prefill_matches_oracle(name, n, mode):
-    """xh_prefill's batched path (prefill.h: hipBLASLt GEMMs over passes of <= 512 tokens for
-    f16 / fp8 weights, MFMA GEMMs over passes of <= 64 tokens otherwise; causal attention per
-    token) vs the oracle's token-by-token HYDRATE loop: last logits, every
-    layer's K and V rows, and the greedy continuation after it.  mode 1: the default choice
-    per dtype; 2: split-f16 MFMA wherever the weights allow (f16 / fp8); 3: f32-input MFMA."""
+    """xh_prefill's batched path (prefill.h / gemm16.h: the LDS-tiled f16 MFMA GEMM over passes of
+    <= 1024 tokens for f16 / fp8 weights, register-streaming MFMA GEMMs over passes of <= 64 tokens
+    otherwise; causal attention on MFMA tiles) vs the oracle's token-by-token HYDRATE loop: last
+    logits, every layer's K and V rows, and the greedy continuation after it.  mode 1: the default
+    choice per dtype; 2: split-f16 register-streaming MFMA wherever the weights allow (f16 / fp8);
+    3: f32-input MFMA; 4: mode 1 with hipBLASLt in place of gemm16.h."""
     xf = XalmFile(fixture_path(name + ".xalm"))
     gm = Model.from_xalm(xf, context=256)
     assert gm.get_option(L.OPT_PREFILL) == 1
@@ -171,16 +172,18 @@ def test_batched_prefill_matches_oracle(name, n, mode):
     check(st.logits(), om.logits(), name, "prefill")
 
 
+@pytest.mark.parametrize("mode,n", [(1, 1200), (4, 700)])
 @pytest.mark.parametrize("name", ["tiny_mistral_f16", "tiny_mistral_f8_e4m3", "small_llama_f16"])
-def test_blas_prefill_multi_pass_matches_oracle(name):
-    """XH_OPT_PREFILL 1 on f16 / fp8 weights: hipBLASLt passes of 512 tokens; 700 tokens = a
-    full pass and a 188-token one (the second attends over the first pass's K/V rows).  Last
-    logits and every layer's K/V rows vs the oracle's token loop, then the perplexity path over
-    600 tokens (lm_head as one hipBLASLt GEMM per pass, or 64-token slices for bf16 lm_heads)."""
+def test_multi_pass_prefill_matches_oracle(name, mode, n):
+    """XH_OPT_PREFILL 1 on f16 / fp8 weights: gemm16.h passes of 1024 tokens (1200 tokens = a full
+    pass and a 176-token one, the second attending over the first pass's K/V rows); 4: hipBLASLt
+    passes of 512 (700 = 512 + 188).  Last logits and every layer's K/V rows vs the oracle's token
+    loop, then the perplexity path over 600 tokens (lm_head as one GEMM per pass, or 64-token
+    slices for bf16 lm_heads)."""
     xf = XalmFile(fixture_path(name + ".xalm"))
-    gm = Model.from_xalm(xf, context=1024)
-    om = O.OracleModel.from_xalm(xf, context=1024)
-    n = 700
+    gm = Model.from_xalm(xf, context=2048)
+    gm.set_option(L.OPT_PREFILL, mode)
+    om = O.OracleModel.from_xalm(xf, context=2048)
     toks = [1] + [3 + (i * 37) % 280 for i in range(n - 1)]
     st = InferenceState(gm.config)
     gm.prefill(toks, 0, st)
@@ -193,9 +196,29 @@ def test_blas_prefill_multi_pass_matches_oracle(name):
             b = om.kv(layer, which)[:n].view(np.float16).astype(np.float32)
             assert np.abs(a - b).max() <= 2e-3 * max(1.0, np.abs(b).max()), (layer, which)
     gm.close()
-    gm2 = Model.from_xalm(xf, context=1024)
-    om2 = O.OracleModel.from_xalm(xf, context=1024)
+    gm2 = Model.from_xalm(xf, context=2048)
+    gm2.set_option(L.OPT_PREFILL, mode)
+    om2 = O.OracleModel.from_xalm(xf, context=2048)
     check_probs(gm2.token_probs(toks[:600]), om2, toks[:600], name)
+
+
+@pytest.mark.parametrize("mode", [1, 4])
+@pytest.mark.parametrize("wdt", [L.F16, L.F8_E4M3])
+def test_prefill_is_deterministic_across_contexts(wdt, mode):
+    """Two fresh contexts prefill the same 300-token prompt to bitwise-equal logits and K/V rows:
+    the GEMMs' summation order is fixed (gemm16.h tiling; hipBLASLt: the heuristic's first
+    algorithm, no run-time timing of candidates)."""
+    toks = [1] + [3 + (i * 37) % 500 for i in range(299)]
+    out = []
+    for _ in range(2):
+        gm, _om = synthetic_pair(wdt, context=512)
+        gm.set_option(L.OPT_PREFILL, mode)
+        st = InferenceState(gm.config)
+        gm.prefill(toks, 0, st)
+        out.append((st.logits().copy(), gm.kv_read(1, 0, 0, len(toks)).copy()))
+        gm.close()
+    assert np.array_equal(out[0][0].view(np.uint32), out[1][0].view(np.uint32))
+    assert np.array_equal(out[0][1], out[1][1])
 
 
 def synthetic_pair(wdt, dim=256, hidden=512, n_layers=2, vocab=512, context=256):
@@ -224,7 +247,7 @@ def synthetic_pair(wdt, dim=256, hidden=512, n_layers=2, vocab=512, context=256)
 
 
 @pytest.mark.parametrize("glu", [1, 0])
-@pytest.mark.parametrize("mode", [1, 2, 3])
+@pytest.mark.parametrize("mode", [1, 2, 3, 4])
 @pytest.mark.parametrize("wdt", [L.F16, L.F8_E4M3, L.F8_E5M2])
 def test_prefill_gemm_paths_on_synthetic_weights(wdt, mode, glu):
     # dims (256 / 512) that take the split-f16 kernel for fp8 too (K % 8E); 100 tokens = a full
@@ -295,7 +318,7 @@ def test_fused_glu_split_is_bit_identical(wdt):
     assert np.array_equal(out[0], out[1]), float(np.abs(out[0] - out[1]).max())
 
 
-@pytest.mark.parametrize("batched", [1, 2, 3])
+@pytest.mark.parametrize("batched", [1, 2, 3, 4])
 def test_batched_prefill_equals_token_loop(batched):
     """Batched and per-token prefill of the same prompt agree (logits and K/V rings)."""
     xf = XalmFile(fixture_path("small_llama_f16.xalm"))
@@ -416,13 +439,13 @@ def check_probs(got, om, toks, fixture=None):
         check_logp(float(abs(np.log(got[pos]) - np.log(ref))), lg, fixture, pos)
 
 
-@pytest.mark.parametrize("prefill", [1, 2, 3, 0])
+@pytest.mark.parametrize("prefill", [1, 2, 3, 4, 0])
 @pytest.mark.parametrize("name", ["tiny_mistral_f16", "tiny_mistral_bf16", "tiny_mistral_f8_e4m3",
                                   "small_llama_f16"])
 def test_perplexity_probs_match_oracle(name, prefill):
     # xh_perplexity: batched passes (prefill 2 / 3 and bf16: 89 tokens = a full 64-token pass + 25;
-    # prefill 1 on f16 / fp8: one hipBLASLt pass; lm_head
-    # as one GEMM per pass) and the token loop (prefill 0)
+    # prefill 1 / 4 on f16 / fp8: one gemm16.h / hipBLASLt pass; lm_head as one GEMM per pass) and
+    # the token loop (prefill 0)
     xf = XalmFile(fixture_path(name + ".xalm"))
     gm = Model.from_xalm(xf, context=256)
     gm.set_option(L.OPT_PREFILL, prefill)
@@ -445,13 +468,19 @@ def test_prefill_option_values():
     xf = XalmFile(fixture_path("tiny_mistral_f16.xalm"))
     gm = Model.from_xalm(xf)
     assert gm.get_option(L.OPT_PREFILL) == 1
-    for v in (0, 2, 3, 1):
+    for v in (0, 2, 3, 4, 1):
         gm.set_option(L.OPT_PREFILL, v)
         assert gm.get_option(L.OPT_PREFILL) == v
-    for bad in (-1, 4):
+    for bad in (-1, 5):
         with pytest.raises(L.XhError):
             gm.set_option(L.OPT_PREFILL, bad)
     assert gm.get_option(L.OPT_PREFILL) == 1
+    # option id 4 (the removed XH_OPT_COL_KV_MAX) is rejected, not reinterpreted
+    with pytest.raises(L.XhError):
+        gm.set_option(4, 0)
+    with pytest.raises(L.XhError):
+        gm.get_option(4)
+    assert L.OPT_PREFILL_ATTN == 5 and gm.get_option(L.OPT_PREFILL_ATTN) == 1
 
 
 def test_perplexity_arguments():

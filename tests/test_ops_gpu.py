@@ -37,14 +37,16 @@ def decoded(w, dtype):
         return flat.view(np.float16).astype(np.float64)
     if dtype == L.BF16:
         return (flat.astype(np.uint32) << 16).view(np.float32).astype(np.float64)
-    return np.array([O.decode(dtype, flat, i) for i in range(flat.size)], dtype=np.float64)
+    # one-byte codes: the oracle's decode of each of the 256 codes, gathered by code
+    codes = np.arange(256, dtype=np.uint8)
+    table = np.array([O.decode(dtype, codes.view(np.int8) if dtype == L.Q8 else codes, i) for i in range(256)],
+                     dtype=np.float64)
+    return table[flat.view(np.uint8)]
 
 
 @pytest.mark.parametrize("dtype", [L.F16, L.BF16, L.F32, L.F8_E4M3, L.F8_E5M2, L.Q8])
 @pytest.mark.parametrize("n,d", [(64, 32), (512, 96), (4096, 64), (1536, 300), (14336, 8)])
 def test_matmul(dtype, n, d):
-    if dtype in (L.F8_E4M3, L.F8_E5M2, L.Q8) and n * d > 300000:
-        pytest.skip("python-side decode too slow for the reference sum at this size")
     rng = np.random.default_rng(n * 7 + d + dtype)
     x = rng.standard_normal(n).astype(np.float32)
     w = rand_weights(rng, dtype, d, n)
@@ -152,3 +154,47 @@ def test_matmul_f8_hw(dtype, n, d):
     wd = decoded(w, dtype).reshape(d, n)
     mag = np.abs(wd) @ np.abs(x.astype(np.float64))
     assert np.all(np.abs(got - cpu) <= 2e-6 * mag + 1e-7), np.abs(got - cpu).max()
+
+
+def split16(x):
+    """prefill_split_kernel's exact f16 hi + lo of rows scaled into [2^14, 2^15) (float64 ref)"""
+    m = np.abs(x).max(axis=1, keepdims=True)
+    s = np.exp2(15 - np.ceil(np.log2(np.where(m > 0, m, 1.0)) + 1e-12))
+    u = (x * s).astype(np.float32)
+    hi = u.astype(np.float16)
+    lo = (u - hi.astype(np.float32)).astype(np.float16)
+    return hi.view(np.uint16), lo.view(np.uint16)
+
+
+@pytest.mark.parametrize("rows,K,n,ks", [(256, 64, 1, 1), (300, 128, 37, 0), (1000, 512, 200, 4), (6144, 4096, 512, 0),
+                                         (4096, 14336, 130, 0), (28672, 4096, 64, 2), (512, 4096, 1100, 1),
+                                         (4096, 4096, 1024, 8)])
+def test_prompt_gemm(rows, K, n, ks):
+    """The prompt-pass GEMM (gemm16.h) vs a float64 sum of the same f16 products: ragged row and
+    token tiles (clamped loads), 1 to 8 K slices, Mistral-7B shapes; |err| <= 1e-5 sum|terms|
+    (f32 accumulation over up to 14336 products), and bitwise equal on a second launch."""
+    rng = np.random.default_rng(rows + K + n)
+    w = (rng.standard_normal((rows, K)) * 0.02).astype(np.float16)
+    x = rng.standard_normal((n, K))
+    xh, xl = split16(x)
+    got = L.op_prompt_gemm(w.view(np.uint16), xh, xl, ks)
+    assert got.shape == (n, rows)
+    assert np.array_equal(got.view(np.uint32), L.op_prompt_gemm(w.view(np.uint16), xh, xl, ks).view(np.uint32))
+    sel = rng.choice(rows, size=min(rows, 96), replace=False)
+    wd = w[sel].astype(np.float64)
+    xd = xh.view(np.float16).astype(np.float64) + xl.view(np.float16).astype(np.float64)
+    ref = xd @ wd.T
+    mag = np.abs(xd) @ np.abs(wd).T
+    err = np.abs(got[:, sel] - ref)
+    assert np.all(err <= 1e-5 * mag + 1e-7), float((err / (mag + 1e-30)).max())
+
+
+def test_prompt_gemm_rejects_bad_shapes():
+    w = np.zeros((64, 96), np.uint16)
+    x = np.zeros((4, 96), np.uint16)
+    with pytest.raises(L.XhError):
+        L.op_prompt_gemm(w, x, x)  # K not a multiple of 64
+    w = np.zeros((64, 128), np.uint16)
+    x = np.zeros((4, 128), np.uint16)
+    with pytest.raises(L.XhError):
+        L.op_prompt_gemm(w, x, x, 4)  # 4 slices of 32

@@ -134,3 +134,31 @@ def test_oracle_ring_mode_runs_past_context():
     for pos in range(40):
         m.forward(3 + (pos * 7) % 200, pos, L.OUTPUT_LOGITS)
         assert np.isfinite(m.logits()).all()
+
+
+@pytest.mark.parametrize("name,t", [("tiny_mistral", "f16"), ("small_llama", "f16"), ("tiny_mistral", "f8_e4m3"),
+                                    ("tiny_mistral", "q4_0")])
+def test_oracle_f64_evaluation(name, t):
+    """xo_set_precision(m, 1) evaluates the same algorithm in double (the yardstick of
+    tests/test_parity_full_gpu.py): on the fixtures it stays within the north-star bar of the f32
+    evaluation at every position, the first layer's fp16 K rows agree to one fp16 ulp, and the f32 evaluation
+    of a fresh model is unaffected (bitwise)."""
+    xf = XalmFile(fixture_path(f"{name}_{t}.xalm"))
+    m32, m64, again = (O.OracleModel.from_xalm(xf) for _ in range(3))
+    m64.set_precision(1)
+    assert m64.set_precision is not None and O._load().xo_precision(m64.m) == 1
+    toks = [1] + [3 + (i * 37) % 280 for i in range(23)]
+    for pos, tok in enumerate(toks):
+        m32.forward(tok, pos)
+        m64.forward(tok, pos)
+        again.forward(tok, pos)
+        a, b = m32.logits(), m64.logits()
+        assert np.abs(a - b).max() <= 1e-3 * max(1.0, float(np.abs(b).max())), pos
+        assert np.array_equal(a.view(np.uint32), again.logits().view(np.uint32))
+    for layer in range(xf.config().n_layers):
+        ka = m32.kv(layer, 0)[:len(toks)].view(np.float16).astype(np.float32)
+        kb = m64.kv(layer, 0)[:len(toks)].view(np.float16).astype(np.float32)
+        if layer == 0:  # one rounding apart at most
+            assert np.all(np.abs(ka - kb) <= np.abs(kb) * 2.0 ** -10 + 2.0 ** -24)
+        else:  # after a layer of differently rounded activations: the GPU tests' K/V bar
+            assert np.abs(ka - kb).max() <= 2e-3 * max(1.0, float(np.abs(kb).max())), layer

@@ -31,7 +31,7 @@ def row_bytes(dtype: int, n: int) -> int:
 OPT_FUSE_ATTN_WO = 1
 OPT_PREFILL = 2
 OPT_PREFILL_GLU_SPLIT = 3
-OPT_PREFILL_ATTN = 4
+OPT_PREFILL_ATTN = 5
 
 # enum xh_tensor_kind
 EMBED, ATTN_NORM, FFN_NORM, WQ, WK, WV, WO, W1, W2, W3, FINAL_NORM, WCLS = range(12)
@@ -84,6 +84,7 @@ _SIGNATURES = {
     "xh_op_rmsnorm": (_I, [_P, _P, _P, _I, _I, ctypes.c_float]),
     "xh_op_rope": (_I, [_P, _I, _I, _I, ctypes.c_float, _I]),
     "xh_op_mha": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I]),
+    "xh_op_prompt_gemm": (_I, [_P, _P, _P, _P, _I, _I, _I, _I]),
     "xh_time_kernel": (_I, [_P, _I, _I, _FP]),
     "xh_kernel_bytes": (_SZ, [_P, _I, _I]),
 }
@@ -147,4 +148,18 @@ def op_mha(kb: np.ndarray, vb: np.ndarray, q: np.ndarray, head_dim: int, kv_len:
     q = np.ascontiguousarray(q, dtype=np.float32)
     out = np.empty(n_heads * head_dim, dtype=np.float32)
     check(lib().xh_op_mha(ptr(out), ptr(kb), ptr(vb), ptr(q), head_dim, kv_len, max_seq_len, n_heads, n_kv_heads))
+    return out
+
+
+def op_prompt_gemm(w: np.ndarray, xh: np.ndarray, xl: np.ndarray, ks: int = 0) -> np.ndarray:
+    """The prompt-pass GEMM (gemm16.h): y[t][r] = sum_k w[r][k] (xh[t][k] + xl[t][k]); w, xh, xl
+    f16 bit patterns (uint16) [rows][K], [n][K]; returns f32 [n][rows]."""
+    w = np.ascontiguousarray(w, dtype=np.uint16)
+    xh = np.ascontiguousarray(xh, dtype=np.uint16)
+    xl = np.ascontiguousarray(xl, dtype=np.uint16)
+    rows, K = w.shape
+    n = xh.shape[0]
+    assert xh.shape == (n, K) and xl.shape == (n, K)
+    out = np.empty((n, rows), dtype=np.float32)
+    check(lib().xh_op_prompt_gemm(ptr(out), ptr(w), ptr(xh), ptr(xl), rows, K, n, ks))
     return out

@@ -1,6 +1,7 @@
 // dt_launch.hip — fused attention + Wo instantiations for one Wo dtype (-DPK_DT=<xh_dtype>).
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdio>
 
 #include "dt_launch.h"
@@ -19,11 +20,14 @@ int aw_go(const AttnArgs& aa, const GemvArgs& ga, int n_kv_heads, int t_max, uns
     const size_t smem = attn_wo_smem_bytes<DT>(HD, QPK, t_max, aa.nsplit, ga.n, aa.n_heads);
     if (smem > 160 * 1024) return XH_E_INVALID;
     auto k = attn_wo_kernel<DT, HD, QPK>;
-    static bool attr = false;
-    if (!attr) {
+    // the LDS limit is a per-device attribute: set once for each device this process launches on
+    static std::atomic<uint64_t> attr{0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return XH_E_HIP;
+    if (!((attr.load() >> dev) & 1u)) {
         if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
             return XH_E_HIP;
-        attr = true;
+        attr.fetch_or(1ull << dev);
     }
     const int blocks = n_kv_heads * aa.nsplit + gemv_blocks<S>(ga.rows, max_waves / S::WAVES);
     hipLaunchKernelGGL(k, dim3(blocks), dim3(AW_THREADS), smem, stream, aa, ga, n_kv_heads, sync, trace);

@@ -17,8 +17,9 @@
 //   gemv<PRO_RMSNORM, EPI_STORE>    final rmsnorm + lm_head -> logits   (OUTPUT_LOGITS)
 //   gemv<PRO_RMSNORM, EPI_LOGITS>   ... + per-workgroup argmax candidates (greedy graph)
 // fuse_level 0 launches attention and Wo separately.  Prompts go through prefill.h unless
-// XH_OPT_PREFILL is 0: passes of 512 tokens whose GEMMs run on hipBLASLt (f16 weights, fp8 through
-// their exact f16 image; split-f16 activations), else passes of 64 tokens on the hand-written MFMA GEMMs.  (Round 2's one-launch engines — persistent,
+// XH_OPT_PREFILL is 0: passes of up to PF_TOK_MM tokens whose GEMMs run on the LDS-tiled MFMA GEMM
+// of gemm16.h (f16 weights, fp8 through their exact f16 image; split-f16 activations), else
+// passes of 64 tokens on the register-streaming MFMA GEMMs of prefill.h.  (Round 2's one-launch engines — persistent,
 // LDS-DMA stream, qkv+attention+Wo, column-form attention — measured slower and were removed;
 // DESIGN.md §4.5 / §4.9 keep the measurements.)
 #include <hip/hip_runtime.h>
@@ -36,6 +37,8 @@
 #include <cstdio>
 #include <cstring>
 #include <map>
+#include <mutex>
+#include <set>
 #include <string>
 #include <thread>
 #include <vector>
@@ -44,6 +47,7 @@
 #include "attention.h"
 #include "gemv.h"
 #include "dt_launch.h"
+#include "gemm16.h"
 #include "prefill.h"
 #include "standalone.h"
 
@@ -120,30 +124,31 @@ struct xh_ctx {
     unsigned* aw_sync = nullptr;
     // batched prefill (prefill.h), buffers allocated on first use
     bool prefill_batched = true;
-    // XH_OPT_PREFILL: 1 = hipBLASLt for f16 / e4m3 / e5m2 weights (fp8 as an exact f16 image),
-    // f32 MFMA otherwise; 2 = split-f16 MFMA wherever the weights convert exactly; 3 = f32 MFMA only
+    // XH_OPT_PREFILL: 1 = the LDS-tiled f16 MFMA GEMM (gemm16.h) for f16 / e4m3 / e5m2 weights (fp8
+    // as an exact f16 image), f32 MFMA otherwise; 2 = split-f16 register-streaming MFMA wherever the
+    // weights convert exactly; 3 = f32 MFMA only; 4 = as 1 with hipBLASLt in place of gemm16.h
     int prefill_gemm = 1;
     int pf_pass = 0;                             // tokens per pass of the current prefill
+    int pf_cap = 0;                              // tokens the pass buffers hold (pf_alloc)
     bool pf_scaled = false;                      // the last pf_gemm's partials carry 1 / s_t (pf_xs)
-    // hipBLASLt (created on the first prompt that uses it): handle, workspace, plans per shape
+    int mm_ok = 0;                               // 0 unchecked, 1 every pass GEMM fits gemm16.h, -1 not
+    // hipBLASLt (XH_OPT_PREFILL 4, created on the first prompt that uses it): handle, workspace, plans per shape
     hipblasLtHandle_t blas = nullptr;
     void* blas_ws = nullptr;
     struct BlasPlan {
         hipblasLtMatmulDesc_t md = nullptr;
         hipblasLtMatrixLayout_t la = nullptr, lb = nullptr, lc = nullptr;
-        std::vector<hipblasLtMatmulAlgo_t> cands;  // the heuristic's candidates (empty: none)
-        int chosen = -1;                            // -1 until the first GEMM
+        std::vector<hipblasLtMatmulAlgo_t> cands;  // the heuristic's candidates (empty: none; [0] is used)
         bool ready = false;
     };
     int blas_ok = 0;  // 0 unprobed, 1 every GEMM shape of the model has an f16 plan, -1 not
     std::map<std::vector<int>, BlasPlan> blas_plans;
-    uint16_t* pf_wdq = nullptr;                  // f16 image of one fp8 matrix for hipBLASLt (pf_blas_probe)
+    uint16_t* pf_wdq = nullptr;                  // f16 image of one fp8 matrix for the f16 GEMMs (pf_prepare)
     size_t pf_wdq_elems = 0;
     bool pf_split_ready = false;                 // pf_norm left the next GEMM's split input
     bool pf_glu_split = true;                    // XH_OPT_PREFILL_GLU_SPLIT: fused GLU -> split input
     bool pf_attn_mfma = true;                    // XH_OPT_PREFILL_ATTN: 1 MFMA tiles, 0 per-token split kernel
-    bool pf_alloc = false;
-    // T = PF_TOK_MAX tokens (the largest pass)
+    // T = pf_cap tokens (the pass length in use; pf_alloc)
     uint16_t* pf_xh = nullptr;                   // [2T][max K] f16 halves of a GEMM input (pf_alloc)
     uint16_t* pf_xl = nullptr;                   // [PF_TOK][max K] the split kernel's lo fragments
     float* pf_xs = nullptr;                      // [T] 1 / row scale
@@ -153,8 +158,10 @@ struct xh_ctx {
     float* pf_h = nullptr;                       // [T][hidden]
     float* pf_part = nullptr;                    // split-K partials [ks][n][rows] (pf_part_floats)
     StepParams* pf_sp = nullptr;                 // [T] per-token attention scalars
+    // the per-token split attention (XH_OPT_PREFILL_ATTN 0 only, allocated on its first use):
     float *pf_po = nullptr, *pf_pml = nullptr;   // [T][nsplit][q_dim], [T][nsplit][n_heads][2]
     int* pf_cnt = nullptr;                       // [T][n_kv_heads] split tickets
+    int pf_po_cap = 0;                           // tokens those hold
     // xh_perplexity: per-token logits of a pass, targets, probabilities (allocated on first use)
     float* pf_logits = nullptr;                  // [T][vocab]
     int* pf_tgt = nullptr;                       // [T]
@@ -220,6 +227,17 @@ hipError_t fill_sync(xh_ctx* ctx, void* dst, int value, size_t bytes) {
     return e != hipSuccess ? e : hipStreamSynchronize(ctx->stream);
 }
 
+// The dynamic-LDS limit of a kernel above 64 KiB (up to the CU's 160 KiB), set once per (kernel,
+// device): the attribute belongs to the device current at the call.
+void ensure_lds(const void* fn, const int bytes = 160 * 1024) {
+    static std::mutex mu;
+    static std::set<std::pair<const void*, int>> done;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return;
+    std::lock_guard<std::mutex> g(mu);
+    if (done.insert({fn, dev}).second) hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+}
+
 // ---------------------------------------------------------------------------------------
 // gemv launch dispatch
 // ---------------------------------------------------------------------------------------
@@ -238,13 +256,7 @@ void launch_gemv_s(const GemvArgs& a, hipStream_t s, int max_waves) {
     const size_t smem = gemv_smem_bytes<DT, S>(a.n);
     const int blocks = gemv_blocks<S>(a.rows, max_waves / S::WAVES);
     auto k = gemv_kernel<DT, PRO, EPI, S>;
-    if (smem > 64 * 1024) {
-        static bool done = false;
-        if (!done) {
-            hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-            done = true;
-        }
-    }
+    if (smem > 64 * 1024) ensure_lds((const void*)k);
     hipLaunchKernelGGL(k, dim3(blocks), dim3(S::THREADS), smem, s, a);
 }
 
@@ -336,13 +348,7 @@ template <int HD, int QPK>
 void launch_attn_t(const AttnArgs& a, int n_kv_heads, int t_max, hipStream_t s) {
     const size_t smem = attn_smem_bytes(HD, QPK, t_max, a.nsplit);
     auto k = attn_split_kernel<HD, QPK>;
-    if (smem > 64 * 1024) {
-        static bool done = false;
-        if (!done) {
-            hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-            done = true;
-        }
-    }
+    if (smem > 64 * 1024) ensure_lds((const void*)k);
     hipLaunchKernelGGL(k, dim3(n_kv_heads, a.nsplit), dim3(ATTN_THREADS), smem, s, a);
 }
 
@@ -643,34 +649,62 @@ constexpr size_t PF_PART_ROWS = 32 * PF_RT16 * PF_WAVE_TARGET;  // >= ks * rows 
 constexpr int PF_CLS_CHUNK = (int)(PF_PART_ROWS / 4);  // lm_head rows per GEMM (ks <= 4 fits the partials)
 constexpr size_t PF_BLAS_WS = 256ull << 20;            // hipBLASLt workspace
 
-// partials buffer: the MFMA kernels' K slices of 64 tokens, or the hipBLASLt GEMM's two halves
-// (hi, lo) of a 512-token pass over the widest matrix
-size_t pf_part_floats(const xh_ctx* ctx) {
+// partials buffer: the register-streaming MFMA kernels' K slices of 64 tokens, or up to 2 T
+// token rows of partials over the widest matrix (gemm16.h K slices: ks * n <= 2 T; hipBLASLt: the
+// hi and lo halves)
+size_t pf_part_floats(const xh_ctx* ctx, const int T) {
     const xh_config& c = ctx->c;
     const int rows = std::max({ctx->q_dim + 2 * ctx->kv_dim, 2 * c.hidden_dim, c.dim, std::min(c.vocab_size, PF_CLS_CHUNK)});
-    return std::max(PF_PART_ROWS * PF_TOK, (size_t)2 * PF_TOK_MAX * rows);
+    return std::max(PF_PART_ROWS * PF_TOK, (size_t)2 * T * rows);
 }
 
-int pf_alloc(xh_ctx* ctx) {
-    if (ctx->pf_alloc) return 0;
+void pf_free(xh_ctx* ctx) {
+    for (void* p : {(void*)ctx->pf_tok, (void*)ctx->pf_x, (void*)ctx->pf_xn, (void*)ctx->pf_q, (void*)ctx->pf_att,
+                    (void*)ctx->pf_h, (void*)ctx->pf_part, (void*)ctx->pf_sp, (void*)ctx->pf_xh, (void*)ctx->pf_xl,
+                    (void*)ctx->pf_xs, (void*)ctx->pf_logits, (void*)ctx->pf_tgt, (void*)ctx->pf_po,
+                    (void*)ctx->pf_pml, (void*)ctx->pf_cnt})
+        hipFree(p);
+    ctx->pf_tok = nullptr; ctx->pf_x = ctx->pf_xn = ctx->pf_q = ctx->pf_att = ctx->pf_h = ctx->pf_part = nullptr;
+    ctx->pf_sp = nullptr; ctx->pf_xh = ctx->pf_xl = nullptr; ctx->pf_xs = nullptr; ctx->pf_logits = nullptr;
+    ctx->pf_tgt = nullptr; ctx->pf_po = ctx->pf_pml = nullptr; ctx->pf_cnt = nullptr;
+    ctx->pf_cap = ctx->pf_po_cap = 0;
+}
+
+// pass buffers for T tokens (kept while later passes fit; a longer pass length reallocates)
+int pf_alloc(xh_ctx* ctx, const int T) {
+    if (ctx->pf_cap >= T) return 0;
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    pf_free(ctx);
     const xh_config& c = ctx->c;
-    const size_t T = PF_TOK_MAX;
+    const size_t t = (size_t)T;
     int rc;
-    if ((rc = dmalloc(ctx, &ctx->pf_tok, T)) || (rc = dmalloc(ctx, &ctx->pf_x, T * c.dim)) ||
-        (rc = dmalloc(ctx, &ctx->pf_xn, T * c.dim)) || (rc = dmalloc(ctx, &ctx->pf_q, T * ctx->q_dim)) ||
-        (rc = dmalloc(ctx, &ctx->pf_att, T * ctx->q_dim)) || (rc = dmalloc(ctx, &ctx->pf_h, T * c.hidden_dim)) ||
-        (rc = dmalloc(ctx, &ctx->pf_part, pf_part_floats(ctx))) || (rc = dmalloc(ctx, &ctx->pf_sp, T)) ||
-        (rc = dmalloc(ctx, &ctx->pf_po, T * ctx->nsplit * ctx->q_dim)) ||
-        (rc = dmalloc(ctx, &ctx->pf_pml, T * ctx->nsplit * c.n_heads * 2)) ||
-        (rc = dmalloc(ctx, &ctx->pf_cnt, T * c.n_kv_heads)))
+    if ((rc = dmalloc(ctx, &ctx->pf_tok, t)) || (rc = dmalloc(ctx, &ctx->pf_x, t * c.dim)) ||
+        (rc = dmalloc(ctx, &ctx->pf_xn, t * c.dim)) || (rc = dmalloc(ctx, &ctx->pf_q, t * ctx->q_dim)) ||
+        (rc = dmalloc(ctx, &ctx->pf_att, t * ctx->q_dim)) || (rc = dmalloc(ctx, &ctx->pf_h, t * c.hidden_dim)) ||
+        (rc = dmalloc(ctx, &ctx->pf_part, pf_part_floats(ctx, T))) || (rc = dmalloc(ctx, &ctx->pf_sp, t)))
         return rc;
-    // pf_xh: the split-kernel fragments of <= 64 tokens, or hi rows then lo rows of a
-    // hipBLASLt pass (one B operand of 2n columns); pf_xl: the split kernel's lo fragments
+    // pf_xh: the split-kernel fragments of <= 64 tokens, or hi rows then lo rows of a row-major
+    // pass input (gemm16.h / hipBLASLt); pf_xl: the split kernel's lo fragments
     const size_t kmax = std::max({(size_t)c.dim, (size_t)c.hidden_dim, (size_t)ctx->q_dim});
-    if ((rc = dmalloc(ctx, &ctx->pf_xh, 2 * T * kmax)) || (rc = dmalloc(ctx, &ctx->pf_xl, PF_TOK * kmax)) ||
-        (rc = dmalloc(ctx, &ctx->pf_xs, T)))
+    if ((rc = dmalloc(ctx, &ctx->pf_xh, 2 * std::max(t, (size_t)PF_TOK) * kmax)) ||
+        (rc = dmalloc(ctx, &ctx->pf_xl, PF_TOK * kmax)) || (rc = dmalloc(ctx, &ctx->pf_xs, std::max(t, (size_t)PF_TOK))))
         return rc;
-    ctx->pf_alloc = true;
+    ctx->pf_cap = T;
+    return 0;
+}
+
+// the per-token split attention's partials (XH_OPT_PREFILL_ATTN 0), sized for the pass
+int pf_alloc_split_attn(xh_ctx* ctx) {
+    if (ctx->pf_po_cap >= ctx->pf_cap) return 0;
+    hipFree(ctx->pf_po); hipFree(ctx->pf_pml); hipFree(ctx->pf_cnt);
+    ctx->pf_po = ctx->pf_pml = nullptr; ctx->pf_cnt = nullptr; ctx->pf_po_cap = 0;
+    const size_t t = (size_t)ctx->pf_cap;
+    int rc;
+    if ((rc = dmalloc(ctx, &ctx->pf_po, t * ctx->nsplit * ctx->q_dim)) ||
+        (rc = dmalloc(ctx, &ctx->pf_pml, t * ctx->nsplit * ctx->c.n_heads * 2)) ||
+        (rc = dmalloc(ctx, &ctx->pf_cnt, t * ctx->c.n_kv_heads)))
+        return rc;
+    ctx->pf_po_cap = ctx->pf_cap;
     return 0;
 }
 
@@ -727,45 +761,17 @@ int blas_plan(xh_ctx* ctx, int rows, int K, int n, xh_ctx::BlasPlan** plan) {
     return 0;
 }
 
-// the GEMM; a full pass (n = 2 PF_TOK_BLAS) first picks the fastest candidate on this very
-// GEMM (its output is rewritten by the real call); other passes take the first candidate
+// the GEMM on the heuristic's first candidate for its shape: a fixed algorithm, so a prompt gives
+// the same logits on every run (no run-time timing of candidates, whose tilings and split-K
+// choices sum in different orders)
 int blas_gemm(xh_ctx* ctx, const void* w, int K, int rows, const uint16_t* x, int n, float* y) {
     xh_ctx::BlasPlan* pp = nullptr;
     int rc = blas_plan(ctx, rows, K, n, &pp);
     if (rc) return rc;
     if (!pp) return set_err(ctx, XH_E_HIP, "hipBLASLt: no algorithm for %d x %d x %d", rows, K, n);
-    xh_ctx::BlasPlan& p = *pp;
     const float alpha = 1.f, beta = 0.f;
-    if (p.chosen < 0) {
-        p.chosen = 0;
-        if (n == 2 * PF_TOK_BLAS && p.cands.size() > 1) {
-            HIP_TRY(ctx, hipGetLastError());  // an earlier launch's error is reported as such
-            hipEvent_t e0, e1;
-            HIP_TRY(ctx, hipEventCreate(&e0));
-            HIP_TRY(ctx, hipEventCreate(&e1));
-            float best = FLT_MAX;
-            for (size_t i = 0; i < p.cands.size(); i++) {
-                float ms = 0.f;
-                bool ok = hipblasLtMatmul(ctx->blas, p.md, &alpha, w, p.la, x, p.lb, &beta, y, p.lc, y, p.lc,
-                                          &p.cands[i], ctx->blas_ws, PF_BLAS_WS, ctx->stream) == HIPBLAS_STATUS_SUCCESS;
-                ok = ok && hipEventRecord(e0, ctx->stream) == hipSuccess;
-                for (int r = 0; ok && r < 3; r++)
-                    ok = hipblasLtMatmul(ctx->blas, p.md, &alpha, w, p.la, x, p.lb, &beta, y, p.lc, y, p.lc,
-                                         &p.cands[i], ctx->blas_ws, PF_BLAS_WS, ctx->stream) == HIPBLAS_STATUS_SUCCESS;
-                ok = ok && hipEventRecord(e1, ctx->stream) == hipSuccess && hipEventSynchronize(e1) == hipSuccess &&
-                     hipEventElapsedTime(&ms, e0, e1) == hipSuccess;
-                if (ok && ms < best) {
-                    best = ms;
-                    p.chosen = (int)i;
-                }
-            }
-            (void)hipGetLastError();  // a candidate that failed to launch is skipped, not reported
-            hipEventDestroy(e0);
-            hipEventDestroy(e1);
-        }
-    }
-    BLAS_TRY(ctx, hipblasLtMatmul(ctx->blas, p.md, &alpha, w, p.la, x, p.lb, &beta, y, p.lc, y, p.lc,
-                                  &p.cands[p.chosen], ctx->blas_ws, PF_BLAS_WS, ctx->stream));
+    BLAS_TRY(ctx, hipblasLtMatmul(ctx->blas, pp->md, &alpha, w, pp->la, x, pp->lb, &beta, y, pp->lc, y, pp->lc,
+                                  &pp->cands[0], ctx->blas_ws, PF_BLAS_WS, ctx->stream));
     return 0;
 }
 
@@ -810,19 +816,22 @@ int pf_elems(int dt) {
     if (dt == XH_F8_E4M3_EXACT || dt == XH_F8_E5M2_EXACT || dt == XH_Q8_0) return 16;
     return dt == XH_Q4_0 ? 32 : elems_per_16b(dt);
 }
-// XH_OPT_PREFILL 1: hipBLASLt runs the GEMM over weights of dtype dt: f16 as stored, e4m3 /
-// e5m2 through their exact f16 image (kdt keeps the _EXACT dtypes, whose NaN / Inf codes the
-// reference decodes to finite values, off this path)
-bool pf_blas(const xh_ctx* ctx, int dt) {
-    if (ctx->prefill_gemm != 1 || (dt != XH_F16 && dt != XH_F8_E4M3 && dt != XH_F8_E5M2)) return false;
-    return ctx->blas_ok > 0;
-}
+// weights the f16 GEMMs take: f16 as stored, e4m3 / e5m2 through their exact f16 image (kdt
+// keeps the _EXACT dtypes, whose NaN / Inf codes the reference decodes to finite values, off it)
 bool pf_f8(int dt) { return dt == XH_F8_E4M3 || dt == XH_F8_E5M2; }
-// Once per context: does hipBLASLt have an f16 plan for every full-pass GEMM of the model?  (If
-// not, every dtype keeps the MFMA kernels: XH_OPT_PREFILL 1's fallback.)  Also sizes the f16
-// image buffer of the largest fp8 matrix.
-int pf_blas_probe(xh_ctx* ctx) {
-    if (ctx->prefill_gemm != 1 || ctx->blas_ok) return 0;
+bool pf_f16w(int dt) { return dt == XH_F16 || pf_f8(dt); }
+// Does the GEMM over W (dtype dt, K columns) run on the row-major split input: gemm16.h
+// (XH_OPT_PREFILL 1: K in whole 64-deep steps) or hipBLASLt (4: a plan for every shape)?
+bool pf_lay0(const xh_ctx* ctx, int dt, int K) {
+    if (!pf_f16w(dt)) return false;
+    if (ctx->prefill_gemm == 1) return K % MM_BK == 0;
+    if (ctx->prefill_gemm == 4) return ctx->blas_ok > 0;
+    return false;
+}
+// Once per prefill: (XH_OPT_PREFILL 4, once per context) does hipBLASLt have an f16 plan for every
+// full-pass GEMM of the model (if not, every dtype keeps the MFMA kernels); and the f16 image
+// buffer of the largest fp8 matrix that goes to the f16 GEMMs.
+int pf_prepare(xh_ctx* ctx) {
     const xh_config& c = ctx->c;
     struct G { int dt, rows, K; };
     std::vector<G> gs;
@@ -833,17 +842,22 @@ int pf_blas_probe(xh_ctx* ctx) {
         gs.push_back({kdt(w.w2_dt, w.w2_x), c.dim, c.hidden_dim});
     }
     gs.push_back({kdt(ctx->wcls_dt, ctx->wcls_x), std::min(PF_CLS_CHUNK, c.vocab_size), c.dim});
-    int ok = 1;
-    size_t wdq = 0;
-    for (const G& g : gs) {
-        if (g.dt != XH_F16 && !pf_f8(g.dt)) continue;
-        xh_ctx::BlasPlan* p = nullptr;
-        int rc = blas_plan(ctx, g.rows, g.K, 2 * PF_TOK_BLAS, &p);
-        if (rc) return rc;
-        if (!p) ok = -1;
-        if (pf_f8(g.dt)) wdq = std::max(wdq, (size_t)g.rows * g.K);
+    if (ctx->prefill_gemm == 4 && !ctx->blas_ok) {
+        int ok = 1;
+        for (const G& g : gs) {
+            if (!pf_f16w(g.dt)) continue;
+            xh_ctx::BlasPlan* p = nullptr;
+            int rc = blas_plan(ctx, g.rows, g.K, 2 * PF_TOK_BLAS, &p);
+            if (rc) return rc;
+            if (!p) ok = -1;
+        }
+        ctx->blas_ok = ok;
     }
-    if (ok > 0 && wdq > ctx->pf_wdq_elems) {
+    size_t wdq = 0;
+    for (const G& g : gs)
+        if (pf_f8(g.dt) && pf_lay0(ctx, g.dt, g.K)) wdq = std::max(wdq, (size_t)g.rows * g.K);
+    if (wdq > ctx->pf_wdq_elems) {
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
         hipFree(ctx->pf_wdq);
         ctx->pf_wdq = nullptr;
         ctx->pf_wdq_elems = 0;
@@ -851,37 +865,39 @@ int pf_blas_probe(xh_ctx* ctx) {
         if (rc) return rc;
         ctx->pf_wdq_elems = wdq;
     }
-    ctx->blas_ok = ok;
     return 0;
 }
-// Layout of the split-f16 input of the GEMM over W (dtype dt, [rows][K]): 0 = row-major (the
-// hipBLASLt path), E > 0 = the split-f16 kernel's fragments, -1 = no split (f32-input MFMA).
-// XH_OPT_PREFILL 1: hipBLASLt for f16 / e4m3 / e5m2 (split kernel for fp8 if hipBLASLt has no
-// plan); 2: the split kernel for f16 and fp8; 3: never split.  The split kernel also needs a K slicing.
+// Layout of the split-f16 input of the GEMM over W (dtype dt, [rows][K]): 0 = row-major (gemm16.h
+// or hipBLASLt), E > 0 = the split-f16 register-streaming kernel's fragments, -1 = no split
+// (f32-input MFMA).  XH_OPT_PREFILL 1 / 4: row-major for f16 / e4m3 / e5m2 where the GEMM fits,
+// else the split kernel for fp8; 2: the split kernel for f16 and fp8; 3: never split.  The split
+// kernel also needs a K slicing.
 int pf_layout(const xh_ctx* ctx, int dt, int K, int rows) {
-    if (pf_blas(ctx, dt)) return 0;
-    const bool f8 = dt == XH_F8_E4M3 || dt == XH_F8_E5M2;
-    if (!(ctx->prefill_gemm == 2 || (ctx->prefill_gemm == 1 && f8))) return -1;
+    if (pf_lay0(ctx, dt, K)) return 0;
+    const bool f8 = pf_f8(dt);
+    const int m = ctx->prefill_gemm;
+    if (!(m == 2 || ((m == 1 || m == 4) && f8))) return -1;
     if (dt != XH_F16 && !f8) return -1;
     const int E = elems_per_16b(dt);
     return pf_ks16(rows, K, E) ? E : -1;
 }
 // split-f16 halves of a pass's rows: hi into pf_xh; lo into pf_xl (fragments) or right after
-// the hi rows (row-major: one B operand of 2n columns)
+// the hi rows (row-major)
 uint16_t* pf_lo(xh_ctx* ctx, int layout, int n, int K) {
     return layout ? ctx->pf_xl : ctx->pf_xh + (size_t)n * K;
 }
 // grid of the split kernels: one workgroup per token row, fragments padded to 32-token tiles
 int pf_split_grid(int layout, int n) { return layout ? 32 * ((n + 31) / 32) : n; }
-// Tokens per pass: 512 when every GEMM of the pass runs on hipBLASLt (the lm_head of a
-// perplexity pass aside: it runs on 64-token slices when it cannot), else 64 (the MFMA kernels'
-// two token tiles)
+// Tokens per pass: PF_TOK_MM (gemm16.h) / PF_TOK_BLAS (hipBLASLt) when every layer GEMM takes the
+// row-major input (the lm_head of a perplexity pass aside: it runs on 64-token slices when it
+// cannot), else 64 (the register-streaming MFMA kernels' two token tiles)
 int pf_pass_tokens(const xh_ctx* ctx) {
+    const xh_config& c = ctx->c;
     for (const LayerW& w : ctx->L)
-        if (!pf_blas(ctx, kdt(w.qkv_dt, w.qkv_x)) || !pf_blas(ctx, kdt(w.wo_dt, w.wo_x)) ||
-            !pf_blas(ctx, kdt(w.w13_dt, w.w13_x)) || !pf_blas(ctx, kdt(w.w2_dt, w.w2_x)))
+        if (!pf_lay0(ctx, kdt(w.qkv_dt, w.qkv_x), c.dim) || !pf_lay0(ctx, kdt(w.wo_dt, w.wo_x), ctx->q_dim) ||
+            !pf_lay0(ctx, kdt(w.w13_dt, w.w13_x), c.dim) || !pf_lay0(ctx, kdt(w.w2_dt, w.w2_x), c.hidden_dim))
             return PF_TOK;
-    return PF_TOK_BLAS;
+    return ctx->prefill_gemm == 4 ? PF_TOK_BLAS : PF_TOK_MM;
 }
 // rmsnorm of the pass's rows (pf_x) as the input of the GEMM over W (dt, [rows][dim]): written
 // straight into the split-f16 halves when that GEMM takes a split input (one launch)
@@ -911,7 +927,7 @@ int pf_gemm(xh_ctx* ctx, const char* what, int dt, const void* w, int K, int row
                                lay, ctx->pf_xh, pf_lo(ctx, lay, n, K), ctx->pf_xs);
     }
     if (lay == 0) {
-        // hi and lo rows as one B operand: partials [2][n][rows], the epilogue scales by 1 / s_t
+        // row-major hi rows then lo rows; partials unscaled, the epilogue multiplies by 1 / s_t
         if (pf_f8(dt)) {
             // the matrix's exact f16 image first (one streaming pass: 1 B read, 2 B written per weight)
             const size_t n16 = (size_t)rows * K / 16;
@@ -926,10 +942,23 @@ int pf_gemm(xh_ctx* ctx, const char* what, int dt, const void* w, int K, int row
                                    (const u32x4*)w, n16, (u32x4*)ctx->pf_wdq);
             w = ctx->pf_wdq;
         }
-        int rc = blas_gemm(ctx, w, K, rows, ctx->pf_xh, 2 * n, ctx->pf_part);
-        if (rc) return rc;
         ctx->pf_scaled = true;
-        ks = 2;
+        if (ctx->prefill_gemm == 4) {
+            // hi and lo rows as one B operand of 2n columns: partials [2][n][rows]
+            int rc = blas_gemm(ctx, w, K, rows, ctx->pf_xh, 2 * n, ctx->pf_part);
+            if (rc) return rc;
+            ks = 2;
+            return 0;
+        }
+        MmArgs a{};
+        a.w = (const uint16_t*)w; a.xh = ctx->pf_xh; a.xl = ctx->pf_xh + (size_t)n * K; a.out = ctx->pf_part;
+        a.rows = rows; a.K = K; a.n = n; a.ks = mm_pick_ks(rows, K, n, 2 * ctx->pf_cap);
+        a.n_rt = mm_row_tiles(rows); a.n_tt = mm_tok_tiles(n);
+        if (a.ks <= 0 || (size_t)a.ks * n * rows > pf_part_floats(ctx, ctx->pf_cap))
+            return set_err(ctx, XH_E_INVALID, "prefill: %s GEMM %d x %d over %d tokens does not fit", what, rows, K, n);
+        ensure_lds((const void*)mm_f16_kernel, MM_LDS);
+        hipLaunchKernelGGL(mm_f16_kernel, dim3(a.n_rt * a.n_tt * a.ks), dim3(MM_THREADS), MM_LDS, ctx->stream, a);
+        ks = a.ks;
         return 0;
     }
     if (lay > 0) {
@@ -979,13 +1008,7 @@ template <int HD, int QPK>
 void pf_attn_t(xh_ctx* ctx, const AttnArgs& a, int n) {
     const size_t smem = attn_smem_bytes(HD, QPK, ctx->t_max, a.nsplit);
     auto k = prefill_attn_kernel<HD, QPK>;
-    if (smem > 64 * 1024) {
-        static bool done = false;
-        if (!done) {
-            hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-            done = true;
-        }
-    }
+    if (smem > 64 * 1024) ensure_lds((const void*)k);
     hipLaunchKernelGGL(k, dim3(ctx->c.n_kv_heads, a.nsplit, n), dim3(ATTN_THREADS), smem, ctx->stream, a,
                        (const StepParams*)ctx->pf_sp, ctx->q_dim, ctx->c.n_kv_heads);
 }
@@ -1005,10 +1028,13 @@ bool pf_attn(xh_ctx* ctx, const AttnArgs& a, int n, int pos0) {
         else return false;
         return true;
     }
-    if (hd == 128 && qpk == 4) pf_attn_t<128, 4>(ctx, a, n);
-    else if (hd == 128 && qpk == 8) pf_attn_t<128, 8>(ctx, a, n);
-    else if (hd == 64 && qpk == 4) pf_attn_t<64, 4>(ctx, a, n);
-    else if (hd == 16 && qpk == 2) pf_attn_t<16, 2>(ctx, a, n);
+    if (pf_alloc_split_attn(ctx)) return false;
+    AttnArgs b = a;
+    b.part_o = ctx->pf_po; b.part_ml = ctx->pf_pml; b.counters = ctx->pf_cnt;
+    if (hd == 128 && qpk == 4) pf_attn_t<128, 4>(ctx, b, n);
+    else if (hd == 128 && qpk == 8) pf_attn_t<128, 8>(ctx, b, n);
+    else if (hd == 64 && qpk == 4) pf_attn_t<64, 4>(ctx, b, n);
+    else if (hd == 16 && qpk == 2) pf_attn_t<16, 2>(ctx, b, n);
     else return false;
     return true;
 }
@@ -1034,15 +1060,15 @@ bool pf_supported(const xh_ctx* ctx, int n, int pos0) {
 int prefill_batched(xh_ctx* ctx, const int* tokens, int n, int pos0, int want_logits, const int* targets = nullptr,
                     float* probs = nullptr) {
     const xh_config& c = ctx->c;
-    int rc = pf_alloc(ctx);
+    int rc = pf_prepare(ctx);
     if (rc) return rc;
+    const int pass = ctx->pf_pass = pf_pass_tokens(ctx);
+    if ((rc = pf_alloc(ctx, std::min(pass, std::max(n, PF_TOK))))) return rc;
     ctx->pf_split_ready = false;
     if (probs && !ctx->pf_logits &&
-        ((rc = dmalloc(ctx, &ctx->pf_logits, (size_t)PF_TOK_MAX * c.vocab_size)) ||
-         (rc = dmalloc(ctx, &ctx->pf_tgt, (size_t)PF_TOK_MAX))))
+        ((rc = dmalloc(ctx, &ctx->pf_logits, (size_t)ctx->pf_cap * c.vocab_size)) ||
+         (rc = dmalloc(ctx, &ctx->pf_tgt, (size_t)ctx->pf_cap))))
         return rc;
-    if ((rc = pf_blas_probe(ctx))) return rc;
-    const int pass = ctx->pf_pass = pf_pass_tokens(ctx);
     std::vector<StepParams> sps(pass);
     for (int off = 0; off < n; off += pass) {
         const int m = std::min(n - off, pass);
@@ -1075,9 +1101,8 @@ int prefill_batched(xh_ctx* ctx, const int* tokens, int n, int pos0, int want_lo
             e.head_dim = c.head_dim; e.rope_freq = ctx->rope_freq; e.qkv_clip = c.qkv_clip; e.pos0 = p0; e.act = c.act;
             pf_epi(ctx, e);
             AttnArgs aa = attn_args(ctx, l);
-            aa.q = ctx->pf_q; aa.out = ctx->pf_att; aa.part_o = ctx->pf_po; aa.part_ml = ctx->pf_pml;
+            aa.q = ctx->pf_q; aa.out = ctx->pf_att;
             // splits for this pass's longest row (attn_block: >= ATTN_MIN_T slots per split)
-            aa.counters = ctx->pf_cnt;
             aa.nsplit = std::min(ctx->nsplit, std::max(1, (p0 + m + ATTN_MIN_T - 1) / ATTN_MIN_T));
             if (!pf_attn(ctx, aa, m, p0)) return set_err(ctx, XH_E_INVALID, "prefill: head shape not instantiated");
             if ((rc = pf_gemm(ctx, "wo", kdt(w.wo_dt, w.wo_x), w.wo, ctx->q_dim, c.dim, ctx->pf_att, m, ks))) return rc;
@@ -1126,7 +1151,7 @@ int prefill_batched(xh_ctx* ctx, const int* tokens, int n, int pos0, int want_lo
             const size_t cls_rb = dev_row_bytes(ctx->wcls_dt, c.dim);
             const int cls_dt = kdt(ctx->wcls_dt, ctx->wcls_x);
             // lm_head weights off the hipBLASLt path (bf16 on the fp8 checkpoints): 64-token slices
-            const int tstep = pf_blas(ctx, cls_dt) ? m : PF_TOK;
+            const int tstep = pf_lay0(ctx, cls_dt, c.dim) ? m : PF_TOK;
             for (int r0 = 0; r0 < c.vocab_size; r0 += PF_CLS_CHUNK) {
                 const int rows = std::min(PF_CLS_CHUNK, c.vocab_size - r0);
                 for (int t0 = 0; t0 < m; t0 += tstep) {
@@ -1299,10 +1324,8 @@ void xh_destroy(xh_ctx* ctx) {
     hipFree(ctx->embed); hipFree(ctx->final_norm);
     hipFree(ctx->kv); hipFree(ctx->x); hipFree(ctx->q); hipFree(ctx->attn_out); hipFree(ctx->hb);
     hipFree(ctx->logits); hipFree(ctx->part_o); hipFree(ctx->part_ml); hipFree(ctx->attn_cnt); hipFree(ctx->aw_sync); hipFree(ctx->cand); hipFree(ctx->scan_flag);
-    hipFree(ctx->pf_tok); hipFree(ctx->pf_x); hipFree(ctx->pf_xn); hipFree(ctx->pf_q); hipFree(ctx->pf_att); hipFree(ctx->pf_h);
-    hipFree(ctx->pf_xh); hipFree(ctx->pf_xl); hipFree(ctx->pf_xs); hipFree(ctx->pf_wdq);
-    hipFree(ctx->pf_logits); hipFree(ctx->pf_tgt); hipFree(ctx->ppl_tgt); hipFree(ctx->ppl_prob);
-    hipFree(ctx->pf_part); hipFree(ctx->pf_sp); hipFree(ctx->pf_po); hipFree(ctx->pf_pml); hipFree(ctx->pf_cnt); hipFree(ctx->rope_freq);
+    pf_free(ctx);
+    hipFree(ctx->pf_wdq); hipFree(ctx->ppl_tgt); hipFree(ctx->ppl_prob); hipFree(ctx->rope_freq);
     hipFree(ctx->aw_trace);
     for (auto& kv : ctx->blas_plans) {
         const xh_ctx::BlasPlan& p = kv.second;
@@ -1860,7 +1883,7 @@ int xh_set_option(xh_ctx* ctx, int option, int value) {
             drop_graphs(ctx);
             return 0;
         case XH_OPT_PREFILL:
-            if (value < 0 || value > 3) return set_err(ctx, XH_E_INVALID, "XH_OPT_PREFILL: 0 ... 3");
+            if (value < 0 || value > 4) return set_err(ctx, XH_E_INVALID, "XH_OPT_PREFILL: 0 ... 4");
             ctx->prefill_batched = value != 0;
             if (value) ctx->prefill_gemm = value;
             return 0;
@@ -1986,6 +2009,36 @@ int xh_op_mha(float* xout, const uint16_t* kb, const uint16_t* vb, const float* 
     if (!launch_attn(a, head_dim, qpk, n_kv_heads, t_max, nullptr))
         return set_err(nullptr, XH_E_INVALID, "unsupported head_dim %d / qpk %d", head_dim, qpk);
     return op_finish(xout, bo, (size_t)n_heads * head_dim * 4);
+}
+
+int xh_op_prompt_gemm(float* y, const uint16_t* w, const uint16_t* xh, const uint16_t* xl, int rows, int K, int n,
+                      int ks) {
+    if (!y || !w || !xh || !xl || rows <= 0 || n <= 0 || K <= 0 || K % MM_BK || ks < 0 || ks > 64)
+        return set_err(nullptr, XH_E_INVALID, "bad prompt_gemm args");
+    if (ks == 0) ks = mm_pick_ks(rows, K, n, 2 * PF_TOK_MM);
+    if (K % (ks * MM_BK)) return set_err(nullptr, XH_E_INVALID, "K %d not in %d slices of 64", K, ks);
+    DevBuf bw, bx, bo;
+    int rc;
+    const size_t xe = (size_t)n * K;
+    if ((rc = op_alloc(bw, (size_t)rows * K * 2, w)) || (rc = op_alloc(bx, 2 * xe * 2, nullptr)) ||
+        (rc = op_alloc(bo, (size_t)ks * n * rows * 4, nullptr)))
+        return rc;
+    if (hipMemcpy(bx.p, xh, xe * 2, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy((uint16_t*)bx.p + xe, xl, xe * 2, hipMemcpyHostToDevice) != hipSuccess)
+        return set_err(nullptr, XH_E_HIP, "hipMemcpy failed");
+    MmArgs a{};
+    a.w = (const uint16_t*)bw.p; a.xh = (const uint16_t*)bx.p; a.xl = (const uint16_t*)bx.p + xe; a.out = (float*)bo.p;
+    a.rows = rows; a.K = K; a.n = n; a.ks = ks; a.n_rt = mm_row_tiles(rows); a.n_tt = mm_tok_tiles(n);
+    ensure_lds((const void*)mm_f16_kernel, MM_LDS);
+    hipLaunchKernelGGL(mm_f16_kernel, dim3(a.n_rt * a.n_tt * ks), dim3(MM_THREADS), MM_LDS, nullptr, a);
+    std::vector<float> part((size_t)ks * n * rows);
+    if ((rc = op_finish(part.data(), bo, part.size() * 4))) return rc;
+    for (size_t i = 0; i < (size_t)n * rows; i++) {
+        float v = 0.f;
+        for (int s = 0; s < ks; s++) v += part[(size_t)s * n * rows + i];  // slice order, as prefill_epi_kernel
+        y[i] = v;
+    }
+    return 0;
 }
 
 // ---------------------------------------------------------------------------------------
