@@ -165,29 +165,56 @@ def host_cpu_info():
     return info
 
 
+def usable_physical_cores():
+    """Physical cores (distinct package / core ids) among the CPUs in this process's affinity
+    mask, capped by a cgroup CPU quota if one is set: the cores a `-d cpu` run here can use
+    (BASELINE.md §3 asks for OMP_NUM_THREADS = all physical cores)."""
+    cpus = sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else list(range(os.cpu_count() or 1))
+    phys = set()
+    for c in cpus:
+        try:
+            with open(f"/sys/devices/system/cpu/cpu{c}/topology/physical_package_id") as f:
+                pkg = f.read().strip()
+            with open(f"/sys/devices/system/cpu/cpu{c}/topology/core_id") as f:
+                core = f.read().strip()
+            phys.add((pkg, core))
+        except OSError:
+            phys.add(("cpu", c))
+    n, quota = len(phys), None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+            n = min(n, max(1, int(quota)))
+    except (OSError, ValueError):
+        pass
+    return max(1, n), quota
+
+
 def progress(msg):
     """A progress line on stderr (the JSON result is the only stdout line)."""
     print(msg, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(w, c, prompt, gpu_logits0, gpu_tokens, n_decode, one_thread_tokens=2):
+def cpu_baseline(w, c, prompt, gpu_logits0, gpu_tokens, n_decode, one_thread_tokens=2, share_tokens=8):
     """The reference -d cpu path (the oracle: src/infer.cpp restated, OpenMP over matvec rows and
-    heads as src/infer.cpp:118 / :438) on the same synthetic weights, timed on this host: hydrate
-    the prompt, then `n_decode` decode tokens teacher-forced on the GPU's tokens (run_completion
-    -m completion -n N, src/main.cpp:94-115), as wall tok/s and as the reference's own statistic
-    (prompt + generated) / (user + sys CPU s) (src/main.cpp:117-127, src/profiler.h:124-129; NOT
-    wall clock).  Parity of the same run: GPU logits after the prompt vs the oracle's, next to
-    the oracle's own sensitivity to the in-row summation order (8-wide FMA lanes vs sequential,
-    both valid readings of the reference's `omp simd` loop)."""
+    heads as src/infer.cpp:118 / :438) on the same synthetic weights, timed on this host with
+    OpenMP threads = the physical cores this process may use: hydrate the prompt,
+    then `n_decode` decode tokens teacher-forced on the GPU's tokens (run_completion -m completion
+    -n N, src/main.cpp:94-115), as wall tok/s and as the reference's own statistic (prompt +
+    generated) / (user + sys CPU s) (src/main.cpp:117-127, src/profiler.h:124-129; NOT wall
+    clock).  Beside it: the same decode at the GPU box's CPU share (OMP_NUM_THREADS as set for the
+    job) and on one thread.  Parity of the same run: GPU logits after the prompt against the
+    oracle's f32 evaluation and against the fp64 evaluation of the same algorithm
+    (xo_set_precision), with the f32 evaluation's own distance from the fp64 one."""
     import resource
 
     from oracle import oracle as O
     t_gen = time.time()
     weights = [(kind, layer, dt, O.synthetic(*tensor_shape(c, kind), dt, seed, mean, std))
                for kind, layer, dt, seed, mean, std in tensor_specs(w)]
-    om = O.OracleModel(c)
-    for kind, layer, dt, arr in weights:
-        om.set_tensor(kind, layer, dt, arr)
+    kv_rows = []
     pos0, hyd = 0, prompt
     if w["kv_prefill"]:
         kv_dim = c.n_kv_heads * c.head_dim
@@ -195,26 +222,38 @@ def cpu_baseline(w, c, prompt, gpu_logits0, gpu_tokens, n_decode, one_thread_tok
             if layer % 8 == 0:
                 progress(f"cpu baseline: KV history layer {layer} / {c.n_layers}")
             for which in (0, 1):
-                om.set_kv(layer, which, 0, O.synthetic(w["kv_prefill"], kv_dim, L.F16, 5000 + 2 * layer + which,
-                                                       0.0, 1.0))
+                kv_rows.append((layer, which, O.synthetic(w["kv_prefill"], kv_dim, L.F16, 5000 + 2 * layer + which,
+                                                          0.0, 1.0)))
         pos0, hyd = w["kv_prefill"], prompt[:1]
+
+    def oracle(prec=0):
+        om = O.OracleModel(c)
+        for kind, layer, dt, arr in weights:
+            om.set_tensor(kind, layer, dt, arr)
+        for layer, which, arr in kv_rows:
+            om.set_kv(layer, which, 0, arr)
+        om.set_precision(prec)
+        return om
+
+    om = oracle()
     t_gen = time.time() - t_gen
     progress(f"cpu baseline: weights ready ({t_gen:.1f} s)")
-    threads = O.num_threads()
+    share = O.num_threads()  # the job's OMP_NUM_THREADS (the GPU box's CPU share)
+    cores, quota = usable_physical_cores()
+    O.set_threads(cores)
     ru0 = resource.getrusage(resource.RUSAGE_SELF)
     t0 = time.time()
     for i, tok in enumerate(hyd):
         om.forward(tok, pos0 + i, L.OUTPUT_LOGITS if i == len(hyd) - 1 else L.HYDRATE_KV_CACHE)
     t_hyd = time.time() - t0
     lg0 = om.logits()
-    parity_max_abs = float(np.abs(lg0 - gpu_logits0).max())
     # teacher-forced on the GPU's tokens so both sides see identical inputs
     pos = pos0 + len(hyd)
     agree, disagree = 0, []
     t1 = time.time()
     for i in range(n_decode):
-        if i % 8 == 0:
-            progress(f"cpu baseline: decode token {i} / {n_decode}")
+        if i % 16 == 0:
+            progress(f"cpu baseline: decode token {i} / {n_decode} ({cores} threads)")
         lg = om.logits()
         ref_tok = O.sample_argmax(lg)
         if ref_tok == gpu_tokens[i]:
@@ -227,36 +266,39 @@ def cpu_baseline(w, c, prompt, gpu_logits0, gpu_tokens, n_decode, one_thread_tok
     t_dec = time.time() - t1
     ru1 = resource.getrusage(resource.RUSAGE_SELF)
     cpu_s = (ru1.ru_utime - ru0.ru_utime) + (ru1.ru_stime - ru0.ru_stime)
-    # one-thread sample: a couple more teacher-forced tokens on one thread
-    O.set_threads(1)
+
+    nxt = n_decode  # the next teacher-forcing token
+
+    def sample(threads, n_tok):
+        nonlocal pos, nxt
+        O.set_threads(threads)
+        t = time.time()
+        for _ in range(n_tok):
+            om.forward(gpu_tokens[nxt], pos, L.OUTPUT_LOGITS)
+            pos += 1
+            nxt += 1
+        return n_tok / (time.time() - t)
+
+    # the job's CPU share and one thread, a few more teacher-forced tokens each
+    share_tps = sample(share, share_tokens) if share != cores else n_decode / t_dec
+    one_tps = sample(1, one_thread_tokens)
+    O.set_threads(cores)
+    om.close()
+    # fp64 evaluation of the same prompt (the algorithm's value independent of f32 rounding order)
     t2 = time.time()
-    for i in range(one_thread_tokens):
-        om.forward(gpu_tokens[n_decode + i], pos, L.OUTPUT_LOGITS)
-        pos += 1
-    one = (time.time() - t2) / one_thread_tokens
-    O.set_threads(threads)
-    # order sensitivity: the same prompt on a fresh oracle with sequential in-row sums (the
-    # prompt only: a 32k history is the same rows either way)
-    order = None
-    if not w["kv_prefill"] and w["wdt"] == L.F16:
-        om.close()
-        om2 = O.OracleModel(c)
-        for kind, layer, dt, arr in weights:
-            om2.set_tensor(kind, layer, dt, arr)
-        O.set_matmul_order(1)
-        for i, tok in enumerate(hyd):
-            om2.forward(tok, i, L.OUTPUT_LOGITS if i == len(hyd) - 1 else L.HYDRATE_KV_CACHE)
-        O.set_matmul_order(0)
-        lg_seq = om2.logits()
-        om2.close()
-        order = {"oracle_lanes_vs_sequential_max_abs": float(np.abs(lg0 - lg_seq).max()),
-                 "gpu_vs_oracle_sequential_max_abs": float(np.abs(gpu_logits0 - lg_seq).max())}
+    om64 = oracle(1)
+    for i, tok in enumerate(hyd):
+        om64.forward(tok, pos0 + i, L.OUTPUT_LOGITS if i == len(hyd) - 1 else L.HYDRATE_KV_CACHE)
+    lg64 = om64.logits()
+    om64.close()
+    t_64 = time.time() - t2
+    O.set_threads(share)
     cpu = host_cpu_info()
-    return dict(value=round(n_decode / t_dec, 3), unit="tok/s", cores=threads, kind="port",
+    return dict(value=round(n_decode / t_dec, 3), unit="tok/s", cores=cores, kind="port",
                 cpu_model=cpu["model"], host_physical_cores=cpu["physical_cores"],
-                host_logical_cpus=cpu["logical_cpus"], affinity_cpus=cpu["affinity_cpus"],
-                threads_note="OpenMP threads = this process's CPU share on the GPU box (OMP_NUM_THREADS / "
-                             "affinity), not the host's physical core count",
+                host_logical_cpus=cpu["logical_cpus"], affinity_cpus=cpu["affinity_cpus"], cgroup_cpu_quota=quota,
+                threads_note="OpenMP threads = the physical cores in this process's affinity mask (capped by a "
+                             "cgroup quota if set), BASELINE.md §3",
                 sample=f"-m completion -n {n_decode} equivalent: {len(hyd)}-token hydrate"
                        + (f" at pos {pos0} over a {w['kv_prefill']}-slot history" if w["kv_prefill"] else "")
                        + f", then {n_decode} greedy decode tokens teacher-forced on the GPU's tokens, full "
@@ -268,11 +310,19 @@ def cpu_baseline(w, c, prompt, gpu_logits0, gpu_tokens, n_decode, one_thread_tok
                                 "unit": "tok/s", "definition": "(prompt + generated) / (user + sys CPU s), "
                                 "src/main.cpp:117-127 + src/profiler.h:124-129; NOT wall clock",
                                 "user_sys_s": round(cpu_s, 2)},
-                one_thread={"value": round(1.0 / one, 3), "unit": "tok/s", "cores": 1,
+                job_share={"value": round(share_tps, 3), "unit": "tok/s", "cores": share,
+                           "sample": f"{share_tokens if share != cores else n_decode} teacher-forced decode tokens at "
+                                     "the job's OMP_NUM_THREADS"},
+                one_thread={"value": round(one_tps, 3), "unit": "tok/s", "cores": 1,
                             "sample": f"{one_thread_tokens} teacher-forced decode tokens"},
-                parity={"logits_max_abs_after_prompt": parity_max_abs,
-                        "logits_scale": float(np.abs(lg0).max()),
-                        "order_sensitivity": order,
+                parity={"gpu_vs_oracle32_max_abs": float(np.abs(lg0 - gpu_logits0).max()),
+                        "gpu_vs_oracle64_max_abs": float(np.abs(lg64 - gpu_logits0).max()),
+                        "oracle32_vs_oracle64_max_abs": float(np.abs(lg64 - lg0).max()),
+                        "logits_scale": float(np.abs(lg64).max()),
+                        "note": "logits after the prompt; oracle64 = the same algorithm evaluated in double "
+                                "(fp16 K/V cache kept); the GPU passes when it is no further from oracle64 than "
+                                "the reference's own f32 evaluation (tests/test_parity_full_gpu.py)",
+                        "oracle64_s": round(t_64, 1),
                         "greedy_tokens_agree": f"{agree}/{n_decode}", "disagreements": disagree[:16]})
 
 
@@ -286,9 +336,10 @@ def main():
                     help="CPU baseline decode tokens (-m completion -n N; 32k workload: min(N, 32))")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--kernel-iters", type=int, default=200)
-    ap.add_argument("--prefill-mode", type=int, default=1, choices=(1, 2, 3),
-                    help="batched prefill GEMMs (XH_OPT_PREFILL): 1 default per dtype (hipBLASLt for f16 / "
-                         "fp8 weights), 2 split-f16 MFMA wherever the weights allow, 3 f32-input MFMA only")
+    ap.add_argument("--prefill-mode", type=int, default=1, choices=(1, 2, 3, 4),
+                    help="batched prefill GEMMs (XH_OPT_PREFILL): 1 default per dtype (the LDS-tiled f16 MFMA "
+                         "GEMM of gemm16.h for f16 / fp8 weights), 2 split-f16 register-streaming MFMA wherever "
+                         "the weights allow, 3 f32-input MFMA only, 4 as 1 on vendor hipBLASLt")
     ap.add_argument("--prefill-tokens", type=int, default=2048,
                     help="also time xh_prefill of this many prompt tokens (batched path; 0 = skip)")
     ap.add_argument("--fuse-attn-wo", type=int, default=1, choices=(0, 1),
@@ -335,6 +386,15 @@ def main():
 
     toks, elapsed = timed_region(dist, torch_mod, lambda: model.decode_greedy(pos, args.steps))
     assert len(toks) == args.steps
+    # the CPU baseline's teacher-forcing tokens beyond the timed ones (-n 128 whatever --steps is):
+    # the same greedy sequence continued on the device, untimed
+    cpu_n = 0
+    extra = []
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu_n = min(args.cpu_tokens, 32) if w["kv_prefill"] else args.cpu_tokens
+        need = cpu_n + 2 + 8 - (args.warmup + args.steps)
+        if need > 0 and (w["kv_prefill"] or pos + args.steps + need <= c.max_seq_len):
+            extra = model.decode_greedy(pos + args.steps, need)
 
     # algorithmic bytes of the timed tokens: Model::active_bytes(pos) (src/model.cpp:12-35)
     step_bytes = sum(model.active_bytes(p) for p in range(pos, pos + args.steps))
@@ -355,9 +415,7 @@ def main():
     # prompt processing, reported beside the decode metric: xh_prefill of a
     # synthetic prompt at positions 0.. (overwrites the ring rows the decode used; timed last)
     prefill = None
-    # the MFMA prompt path has no gguf-block GEMM (those models hydrate token by token)
-    batched_ok = w["wdt"] not in L.GQ_BLOCK_BYTES
-    if args.prefill_tokens and batched_ok and not w["kv_prefill"] and args.prefill_tokens <= c.max_seq_len:
+    if args.prefill_tokens and not w["kv_prefill"] and args.prefill_tokens <= c.max_seq_len:
         ptoks = prompt_tokens(c.vocab_size, n=args.prefill_tokens, seed=11)
         model.set_option(L.OPT_PREFILL, args.prefill_mode)
         model.prefill(ptoks, 0, st)  # warm: buffers, code objects, hipBLASLt plans
@@ -371,12 +429,14 @@ def main():
         flops = 2.0 * args.prefill_tokens * c.n_layers * layer_params  # matrix products only
         prefill = {"tokens": args.prefill_tokens, "ms": round(pf_s * 1e3, 2),
                    "tok_s": round(args.prefill_tokens / pf_s, 1),
-                   "mode": {0: "per-token", 1: "batched (hipBLASLt for f16 / fp8 weights, else MFMA kernels)",
-                            2: "batched split-f16 MFMA", 3: "batched f32-input MFMA"}[model.get_option(L.OPT_PREFILL)],
-                   "note": "f16 / fp8 weights: passes of 512 tokens, hipBLASLt f16 GEMMs (fp8 matrices through their "
-                           "exact f16 image) over f16 hi+lo activation pairs (power-of-two row scale, ~22-bit "
-                           "mantissa); other dtypes: passes of 64 tokens on "
-                           "the hand-written MFMA GEMMs (f32 activations as the reference, or split-f16)",
+                   "mode": {0: "per-token", 1: "batched: gemm16.h LDS-tiled f16 MFMA GEMM (f16 / fp8 weights), "
+                                               "else register-streaming MFMA kernels",
+                            2: "batched split-f16 register-streaming MFMA", 3: "batched f32-input MFMA",
+                            4: "batched: hipBLASLt f16 GEMMs (f16 / fp8 weights)"}[model.get_option(L.OPT_PREFILL)],
+                   "note": "f16 / fp8 weights: passes of up to 1024 tokens (hipBLASLt: 512), f16 GEMMs (fp8 matrices "
+                           "through their exact f16 image) over f16 hi+lo activation pairs (power-of-two row scale, "
+                           "~22-bit mantissa), hi and lo accumulated in f32; other dtypes (bf16, gguf blocks): passes "
+                           "of 64 tokens on the register-streaming MFMA GEMMs (f32 activations as the reference)",
                    "matmul_tflops": round(flops / pf_s / 1e12, 1)}
         # run_perplexity's loop (xh_perplexity): the same tokens, every token's logits and
         # sample_prob of the next one on the device
@@ -389,9 +449,9 @@ def main():
                                  "finite": bool(np.isfinite(np.log(probs)).all())}
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        seq = list(warm_tokens) + list(toks)  # the GPU's greedy tokens after the prompt
-        n = min(args.cpu_tokens, 32 if w["kv_prefill"] else args.cpu_tokens, len(seq) - 2)  # +2: 1-thread
+    if cpu_n:
+        seq = list(warm_tokens) + list(toks) + list(extra)  # the GPU's greedy tokens after the prompt
+        n = min(cpu_n, len(seq) - 2 - 8)  # + 2 one-thread tokens + 8 at the job's thread count
         if n > 0:
             cpu = cpu_baseline(w, c, prompt, logits0, seq, n)
 

@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 #include <hipblaslt/hipblaslt.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -21,7 +22,7 @@
 static uint16_t f2h(float f) { _Float16 h = (_Float16)f; uint16_t u; memcpy(&u, &h, 2); return u; }
 static float h2f(uint16_t u) { _Float16 h; memcpy(&h, &u, 2); return (float)h; }
 
-static int pick_ks(int rows, int n, int K) { return xalm::mm_pick_ks(rows, K, n, 4096); }
+static int pick_ks(int rows, int n, int K) { return xalm::mm_pick_ks(rows, K, n, (size_t)2 * 2048 * 28672); }
 
 static float blaslt_us(hipblasLtHandle_t h, int rows, int K, int n2, void* W, void* X, float* Y, void* ws, size_t wss) {
     hipblasLtMatmulDesc_t md;
@@ -84,7 +85,17 @@ int main(int argc, char** argv) {
     const size_t wss = 256ull << 20;
     CK(hipMalloc(&ws, wss));
     CK(hipMemcpy(dw, hw.data(), wmax * 2, hipMemcpyHostToDevice));
-    CK(hipFuncSetAttribute((const void*)xalm::mm_f16_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, xalm::MM_LDS));
+    struct Var { const char* name; void (*fn)(xalm::MmArgs); int lds; };
+    const Var vars[] = {
+        {"bk64", xalm::mm_f16_kernel_t<64, 2, 0>, xalm::MmCfg<64, 2>::LDS},
+        {"bk64pf", xalm::mm_f16_kernel_t<64, 2, 1>, xalm::MmCfg<64, 2>::LDS},
+        {"bk64pri", xalm::mm_f16_kernel_t<64, 2, 2>, xalm::MmCfg<64, 2>::LDS},
+        {"bk64pfpr", xalm::mm_f16_kernel_t<64, 2, 3>, xalm::MmCfg<64, 2>::LDS},
+        {"bk32n4pf", xalm::mm_f16_kernel_t<32, 4, 1>, xalm::MmCfg<32, 4>::LDS},
+    };
+    const int NV = sizeof vars / sizeof vars[0];
+    for (int v = 0; v < NV; v++)
+        CK(hipFuncSetAttribute((const void*)vars[v].fn, hipFuncAttributeMaxDynamicSharedMemorySize, vars[v].lds));
     hipblasLtHandle_t bl;
     CB(hipblasLtCreate(&bl));
     hipEvent_t e0, e1;
@@ -92,7 +103,7 @@ int main(int argc, char** argv) {
     CK(hipEventCreate(&e1));
     int bad = 0;
     for (int n : ns) {
-        double tot_us = 0, tot_bl = 0, tot_flop = 0;
+        double tot_us[8] = {}, tot_bl = 0, tot_flop = 0;
         for (const Shape& sh : shapes) {
             // Xh rows [n][K] then Xl rows [n][K] (the product's layout)
             std::vector<uint16_t> xs(2 * (size_t)n * sh.K);
@@ -107,49 +118,61 @@ int main(int argc, char** argv) {
             a.rows = sh.rows; a.K = sh.K; a.n = n; a.ks = pick_ks(sh.rows, n, sh.K);
             a.n_rt = (sh.rows + xalm::MM_BR - 1) / xalm::MM_BR; a.n_tt = (n + xalm::MM_BT - 1) / xalm::MM_BT;
             const int grid = a.n_rt * a.n_tt * a.ks;
-            auto launch = [&]() {
-                hipLaunchKernelGGL(xalm::mm_f16_kernel, dim3(grid), dim3(xalm::MM_THREADS), xalm::MM_LDS, 0, a);
-            };
-            launch();
-            CK(hipDeviceSynchronize());
-            // check sampled outputs: sum of the ks partials vs a double sum
-            std::vector<float> y((size_t)a.ks * n * sh.rows);
-            CK(hipMemcpy(y.data(), dy, y.size() * 4, hipMemcpyDeviceToHost));
-            double maxrel = 0;
-            std::mt19937 pr(n + sh.rows);
-            for (int smp = 0; smp < 256; smp++) {
-                const int t = pr() % n, r = pr() % sh.rows;
-                double ref = 0, mag = 0;
-                for (int k = 0; k < sh.K; k++) {
-                    const double wv = h2f(hw[(size_t)r * sh.K + k]);
-                    const double xv = (double)h2f(xs[(size_t)t * sh.K + k]) + (double)h2f(xs[((size_t)n + t) * sh.K + k]);
-                    ref += wv * xv;
-                    mag += fabs(wv * xv);
-                }
-                double got = 0;
-                for (int s = 0; s < a.ks; s++) got += y[((size_t)s * n + t) * sh.rows + r];
-                maxrel = fmax(maxrel, fabs(got - ref) / mag);
-            }
-            for (int i = 0; i < 3; i++) launch();
-            CK(hipEventRecord(e0, 0));
-            const int it = 20;
-            for (int i = 0; i < it; i++) launch();
-            CK(hipEventRecord(e1, 0));
-            CK(hipEventSynchronize(e1));
-            float ms = 0;
-            CK(hipEventElapsedTime(&ms, e0, e1));
-            const double us = ms * 1e3 / it;
-            const double flop = 2.0 * sh.rows * sh.K * (double)n;  // counted once (hi + lo = 2x MFMA work)
             const float bus = blaslt_us(bl, sh.rows, sh.K, 2 * n, dw, dx, dy, ws, wss);
-            tot_us += us; tot_bl += bus; tot_flop += flop;
-            const bool ok = maxrel < 2e-6;
-            bad += !ok;
-            printf("n %5d %-4s rows %5d K %5d ks %d grid %4d: %8.1f us = %6.1f TF/s (MFMA %6.1f) | hipBLASLt %8.1f us = %6.1f TF/s | err %.2e %s\n",
-                   n, sh.name, sh.rows, sh.K, a.ks, grid, us, flop / us * 1e-6, 2 * flop / us * 1e-6, bus,
-                   flop / bus * 1e-6, maxrel, ok ? "ok" : "BAD");
+            const double flop = 2.0 * sh.rows * sh.K * (double)n;  // counted once (hi + lo = 2x MFMA work)
+            tot_bl += bus;
+            tot_flop += flop;
+            printf("n %5d %-4s rows %5d K %5d ks %d grid %4d | hipBLASLt %8.1f us = %6.1f TF/s\n", n, sh.name, sh.rows, sh.K,
+                   a.ks, grid, bus, flop / bus * 1e-6);
+            for (int v = 0; v < NV; v++) {
+                auto launch = [&]() {
+                    hipLaunchKernelGGL(vars[v].fn, dim3(grid), dim3(xalm::MM_THREADS), vars[v].lds, 0, a);
+                };
+                CK(hipMemset(dy, 0, (size_t)a.ks * n * sh.rows * 4));
+                launch();
+                CK(hipDeviceSynchronize());
+                // check sampled outputs: sum of the ks partials vs a double sum
+                std::vector<float> y((size_t)a.ks * n * sh.rows);
+                CK(hipMemcpy(y.data(), dy, y.size() * 4, hipMemcpyDeviceToHost));
+                double maxrel = 0;
+                std::mt19937 pr(n + sh.rows);
+                for (int smp = 0; smp < 256; smp++) {
+                    const int t = pr() % n, r = pr() % sh.rows;
+                    double ref = 0, mag = 0;
+                    for (int k = 0; k < sh.K; k++) {
+                        const double wv = h2f(hw[(size_t)r * sh.K + k]);
+                        const double xv = (double)h2f(xs[(size_t)t * sh.K + k]) + (double)h2f(xs[((size_t)n + t) * sh.K + k]);
+                        ref += wv * xv;
+                        mag += fabs(wv * xv);
+                    }
+                    double got = 0;
+                    for (int s = 0; s < a.ks; s++) got += y[((size_t)s * n + t) * sh.rows + r];
+                    maxrel = fmax(maxrel, fabs(got - ref) / mag);
+                }
+                // interleaved rounds (guide rule 24): median of 5 rounds of 10 launches
+                std::vector<float> rounds;
+                for (int i = 0; i < 3; i++) launch();
+                for (int rr = 0; rr < 5; rr++) {
+                    CK(hipEventRecord(e0, 0));
+                    for (int i = 0; i < 10; i++) launch();
+                    CK(hipEventRecord(e1, 0));
+                    CK(hipEventSynchronize(e1));
+                    float ms = 0;
+                    CK(hipEventElapsedTime(&ms, e0, e1));
+                    rounds.push_back(ms * 100.f);
+                }
+                std::sort(rounds.begin(), rounds.end());
+                const double us = rounds[2];
+                tot_us[v] += us;
+                const bool ok = maxrel < 2e-6;
+                bad += !ok;
+                printf("    %-8s %8.1f us = %6.1f TF/s (MFMA %6.1f) err %.2e %s\n", vars[v].name, us, flop / us * 1e-6,
+                       2 * flop / us * 1e-6, maxrel, ok ? "ok" : "BAD");
+            }
         }
-        printf("n %5d layer: %8.1f us = %6.1f TF/s | hipBLASLt %8.1f us = %6.1f TF/s\n", n, tot_us,
-               tot_flop / tot_us * 1e-6, tot_bl, tot_flop / tot_bl * 1e-6);
+        printf("n %5d layer: hipBLASLt %8.1f us = %6.1f TF/s\n", n, tot_bl, tot_flop / tot_bl * 1e-6);
+        for (int v = 0; v < NV; v++)
+            printf("    %-8s %8.1f us = %6.1f TF/s\n", vars[v].name, tot_us[v], tot_flop / tot_us[v] * 1e-6);
     }
     return bad ? 1 : 0;
 }

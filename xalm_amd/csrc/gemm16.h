@@ -14,13 +14,16 @@
 //   * a workgroup owns 256 weight rows x 128 tokens and one K slice (split-K partials
 //     [slice][t][r], summed in slice order by the epilogue); 512 threads = 8 waves as 2 (tokens)
 //     x 4 (rows), each wave 64 tokens x 64 rows = 2 x 2 tiles of 32 x 32 (64 f32 accumulators);
-//   * per K step of 64, the weight tile (256 x 128 B = 32 KiB) and both token tiles (2 x 16 KiB)
-//     go HBM/L2 -> LDS by global_load_lds_dwordx4 (1 KiB per wave-instruction, 8 per wave), into
-//     the second of two 64 KiB LDS stages while the waves multiply the first;
-//   * LDS image: 128-B rows, 16-B chunk c of row r at chunk position c ^ ((r >> 1) & 7), so each
-//     ds_read_b128 lane group (16 distinct rows, one chunk) hits 16 distinct 16-B bank slots (the
-//     DMA writes lane-linearly, so the permutation is applied to the per-lane SOURCE address and
-//     undone on the read);
+//   * per K step of BK, the weight tile (256 rows) and both token tiles (hi, lo: 128 rows each)
+//     go L2 -> LDS by global_load_lds_dwordx4 (1 KiB per wave-instruction) into a ring of NS
+//     stages, NS - 1 steps ahead of the multiply: the wait for step kt is a counted
+//     `s_waitcnt vmcnt` that leaves the later steps' DMA in flight, then a raw s_barrier (a
+//     __syncthreads() would drain every DMA), and the refill goes into the stage every wave
+//     finished reading before that barrier;
+//   * LDS image: rows of BK f16, 16-B chunk c of row r at chunk position c ^ f(r) (f = (r >> 1) & 7
+//     for 8-chunk rows, (r >> 2) & 3 for 4-chunk rows), so each ds_read_b128 lane group (16
+//     distinct rows, one chunk) hits 16 distinct 16-B bank slots (the DMA writes lane-linearly,
+//     so the permutation is applied to the per-lane SOURCE address and undone on the read);
 //   * MFMA operands: A = tokens (lane: token l & 31, k = 8 (l >> 5) + j), B = weight rows (lane:
 //     row l & 31, same k); D lane l holds row l & 31 for tokens (reg & 3) + 8 (reg >> 2) + 4 (l >> 5),
 //     so a store instruction writes 32 consecutive rows (128 B) of two tokens;
@@ -34,10 +37,13 @@ namespace xalm {
 
 constexpr int MM_BR = 256;       // weight rows per workgroup
 constexpr int MM_BT = 128;       // tokens per workgroup
-constexpr int MM_BK = 64;        // k per stage: 128-byte LDS rows
 constexpr int MM_THREADS = 512;  // 8 waves
-constexpr int MM_STAGE = (MM_BR + 2 * MM_BT) * MM_BK * 2;  // bytes: W, Xh, Xl tiles
-constexpr int MM_LDS = 2 * MM_STAGE;                       // 128 KiB
+constexpr int MM_BK = 64;        // k per stage of the default instantiation (mm_f16_kernel below)
+constexpr int MM_NS = 2;         // stages of the default instantiation
+constexpr int MM_FL = 0;         // flags of the default instantiation
+constexpr int MM_KMULT = 64;     // K (and every K slice) in whole multiples of this
+__host__ __device__ constexpr int mm_stage_bytes(const int bk) { return (MM_BR + 2 * MM_BT) * bk * 2; }
+constexpr int MM_LDS = MM_NS * mm_stage_bytes(MM_BK);
 
 typedef _Float16 mm_f16x8 __attribute__((ext_vector_type(8)));
 typedef float mm_f32x16 __attribute__((ext_vector_type(16)));
@@ -47,40 +53,72 @@ struct MmArgs {
     const uint16_t* xh;  // [n][K]
     const uint16_t* xl;  // [n][K]
     float* out;          // [ks][n][rows]
-    int rows, K, n, ks;  // K % (ks * MM_BK) == 0 (host-checked)
+    int rows, K, n, ks;  // K % (ks * BK) == 0 (host-checked)
     int n_rt, n_tt;      // tiles: ceil(rows / MM_BR), ceil(n / MM_BT)
 };
 
 __host__ __device__ constexpr int mm_row_tiles(const int rows) { return (rows + MM_BR - 1) / MM_BR; }
 __host__ __device__ constexpr int mm_tok_tiles(const int n) { return (n + MM_BT - 1) / MM_BT; }
-// K slices: doubled (up to 8) while the grid is under 3/4 of the 256 CUs, K splits into whole
-// 64-deep steps and the partials fit (ks * n <= max_ks_n); 0 if K is not a multiple of MM_BK
-inline int mm_pick_ks(const int rows, const int K, const int n, const int max_ks_n) {
-    if (K % MM_BK) return 0;
+// K slices (1, 2, 4, 8): minimise the modelled time rounds(ks) * (1 / ks + MM_WG_FIXED), rounds =
+// ceil(tiles * ks / n_cu) (workgroups over the CUs) and MM_WG_FIXED a workgroup's fixed cost
+// (prologue, partial stores, tail) in units of one full-K tile, fitted to tools/gemm_bench on
+// MI355X (e.g. qkv at 2048 tokens: 384 tiles are 1.5 rounds, split 2-way 3 even rounds, -7 %;
+// W1/W3 at 512 tokens split 4-way +14 %); K in whole 64-deep steps per slice and
+// ks * n * rows <= max_floats (the partials buffer); 0 if K is not a multiple of 64
+constexpr double MM_WG_FIXED = 0.15;
+inline int mm_pick_ks(const int rows, const int K, const int n, const size_t max_floats, const int n_cu = 256) {
+    if (K % MM_KMULT) return 0;
     const int tiles = mm_row_tiles(rows) * mm_tok_tiles(n);
-    int ks = 1;
-    while (ks < 8 && tiles * ks < 192 && K % (2 * ks * MM_BK) == 0 && 2 * ks * n <= max_ks_n) ks *= 2;
-    return ks;
-}
-
-// byte offset of 16-B chunk c (0..7) of LDS image row r
-__device__ __forceinline__ uint32_t mm_lds_off(const int r, const int c) {
-    return (uint32_t)(r * 128 + 16 * (c ^ ((r >> 1) & 7)));
+    int best = 1;
+    double best_t = 1e30;
+    for (int ks = 1; ks <= 8; ks *= 2) {
+        if (K % (ks * MM_KMULT) || (size_t)ks * n * rows > max_floats) break;
+        const double t = (double)((tiles * ks + n_cu - 1) / n_cu) * (1.0 / ks + MM_WG_FIXED);
+        if (t < best_t * 0.999) {
+            best_t = t;
+            best = ks;
+        }
+    }
+    return best;
 }
 
 typedef __attribute__((address_space(3))) void* mm_lds_ptr;
 
-// One wave-instruction: image rows r0 .. r0 + 7 of a tile from `src` rows (row pitch K elements),
-// lane l -> image row r0 + (l >> 3), chunk position l & 7 (holding source chunk (l & 7) ^ swz).
-__device__ __forceinline__ void mm_issue8(const uint16_t* src_rows, const size_t K, const int r0, const int lane,
-                                          char* lds_tile, const int src_row, const int k) {
-    const int r = r0 + (lane >> 3);
-    const int c = (lane & 7) ^ ((r >> 1) & 7);
-    const uint16_t* g = src_rows + (size_t)src_row * K + k + 8 * c;
-    __builtin_amdgcn_global_load_lds((const void*)g, (mm_lds_ptr)(lds_tile + r0 * 128), 16, 0, 0);
+template <int N>
+__device__ __forceinline__ void mm_wait_vm() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-__global__ __launch_bounds__(MM_THREADS, 2) void mm_f16_kernel(const MmArgs a) {
+template <int BK, int NS>
+struct MmCfg {
+    static constexpr int RB = BK * 2;             // LDS image row bytes
+    static constexpr int CH = RB / 16;            // 16-B chunks per row
+    static constexpr int RPI = 1024 / RB;         // image rows per DMA wave-instruction
+    static constexpr int SH = CH == 8 ? 1 : 2;    // swizzle f(r) = (r >> SH) & (CH - 1)
+    static constexpr int STAGE = mm_stage_bytes(BK);
+    static constexpr int WI = MM_BR / RPI / 8;    // W instructions per wave per stage
+    static constexpr int XI = MM_BT / RPI / 8;    // Xh (and Xl) instructions per wave per stage
+    static constexpr int LPS = WI + 2 * XI;       // DMA instructions per wave per stage
+    static constexpr int LDS = NS * STAGE;
+    static_assert(BK == 32 || BK == 64, "BK");
+    static_assert(NS >= 2 && LDS <= 160 * 1024, "stages");
+    __device__ static uint32_t off(const int r, const int c) { return (uint32_t)(r * RB + 16 * (c ^ ((r >> SH) & (CH - 1)))); }
+};
+
+// the wait before step kt: `ahead` later steps' DMA may stay in flight (ahead = 0 .. NS - 2)
+template <int LPS, int NS>
+__device__ __forceinline__ void mm_wait_ahead(const int ahead) {
+    if constexpr (NS >= 5) { if (ahead >= 3) { mm_wait_vm<3 * LPS>(); return; } }
+    if constexpr (NS >= 4) { if (ahead >= 2) { mm_wait_vm<2 * LPS>(); return; } }
+    if constexpr (NS >= 3) { if (ahead >= 1) { mm_wait_vm<LPS>(); return; } }
+    mm_wait_vm<0>();
+}
+
+// FL bit 0: a k-step's next fragments read before its current MFMAs; bit 1: s_setprio(1) around
+// the MFMA clusters
+template <int BK, int NS, int FL>
+__global__ __launch_bounds__(MM_THREADS, 2) void mm_f16_kernel_t(const MmArgs a) {
+    using C = MmCfg<BK, NS>;
     extern __shared__ __attribute__((aligned(16))) char mm_smem[];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int h = lane >> 5, l32 = lane & 31;
@@ -91,24 +129,45 @@ __global__ __launch_bounds__(MM_THREADS, 2) void mm_f16_kernel(const MmArgs a) {
     const int tt = L % a.n_tt, rest = L / a.n_tt;
     const int s = rest % a.ks, rt = rest / a.ks;
     const int row0 = rt * MM_BR, t0 = tt * MM_BT;
-    const int kslice = a.K / a.ks, kbeg = s * kslice, nk = kslice / MM_BK;
+    const int kslice = a.K / a.ks, kbeg = s * kslice, nk = kslice / BK;
     const size_t K = (size_t)a.K;
 
-    // this lane's source rows for its 8 DMA instructions per stage (clamped: rows / tokens past
-    // the end load valid memory whose products are never stored)
-    int wsrc[4], xsrc[2];
+    // this lane's DMA sources (rows / tokens past the end clamped: valid memory whose products
+    // are never stored) and chunk: image row r0 + lane / CH, chunk position lane % CH holding
+    // source chunk (lane % CH) ^ f(row)
+    const uint16_t* wsrc[C::WI];
+    const uint16_t* hsrc[C::XI];
+    const uint16_t* lsrc[C::XI];
 #pragma unroll
-    for (int i = 0; i < 4; i++) wsrc[i] = min(row0 + 32 * wv + 8 * i + (lane >> 3), a.rows - 1);
+    for (int i = 0; i < C::WI; i++) {
+        const int r = (wv * C::WI + i) * C::RPI + lane / C::CH;
+        const int c = (lane % C::CH) ^ ((r >> C::SH) & (C::CH - 1));
+        wsrc[i] = a.w + (size_t)min(row0 + r, a.rows - 1) * K + kbeg + 8 * c;
+    }
 #pragma unroll
-    for (int i = 0; i < 2; i++) xsrc[i] = min(t0 + 16 * wv + 8 * i + (lane >> 3), a.n - 1);
-    auto issue = [&](const int stage, const int k) {
-        char* base = mm_smem + stage * MM_STAGE;
+    for (int i = 0; i < C::XI; i++) {
+        const int r = (wv * C::XI + i) * C::RPI + lane / C::CH;
+        const int c = (lane % C::CH) ^ ((r >> C::SH) & (C::CH - 1));
+        const size_t o = (size_t)min(t0 + r, a.n - 1) * K + kbeg + 8 * c;
+        hsrc[i] = a.xh + o;
+        lsrc[i] = a.xl + o;
+    }
+    auto issue = [&](const int stage, const int kt) {
+        char* base = mm_smem + stage * C::STAGE;
+        const int k = kt * BK;
 #pragma unroll
-        for (int i = 0; i < 4; i++) mm_issue8(a.w, K, 32 * wv + 8 * i, lane, base, wsrc[i], k);
+        for (int i = 0; i < C::WI; i++)
+            __builtin_amdgcn_global_load_lds((const void*)(wsrc[i] + k), (mm_lds_ptr)(base + (wv * C::WI + i) * 1024), 16,
+                                             0, 0);
 #pragma unroll
-        for (int i = 0; i < 2; i++) mm_issue8(a.xh, K, 16 * wv + 8 * i, lane, base + MM_BR * 128, xsrc[i], k);
+        for (int i = 0; i < C::XI; i++)
+            __builtin_amdgcn_global_load_lds((const void*)(hsrc[i] + k),
+                                             (mm_lds_ptr)(base + MM_BR * C::RB + (wv * C::XI + i) * 1024), 16, 0, 0);
 #pragma unroll
-        for (int i = 0; i < 2; i++) mm_issue8(a.xl, K, 16 * wv + 8 * i, lane, base + (MM_BR + MM_BT) * 128, xsrc[i], k);
+        for (int i = 0; i < C::XI; i++)
+            __builtin_amdgcn_global_load_lds((const void*)(lsrc[i] + k),
+                                             (mm_lds_ptr)(base + (MM_BR + MM_BT) * C::RB + (wv * C::XI + i) * 1024), 16,
+                                             0, 0);
     };
 
     const int wt = wv >> 2, wr = wv & 3;  // this wave's 64 tokens / 64 rows of the tile
@@ -117,40 +176,63 @@ __global__ __launch_bounds__(MM_THREADS, 2) void mm_f16_kernel(const MmArgs a) {
     for (int i = 0; i < 2; i++)
 #pragma unroll
         for (int j = 0; j < 2; j++) acc[i][j] = mm_f32x16{};
-    auto compute = [&](const int stage) {
-        const char* base = mm_smem + stage * MM_STAGE;
-        const char* wt_img = base;
-        const char* xh_img = base + MM_BR * 128;
-        const char* xl_img = base + (MM_BR + MM_BT) * 128;
+    struct Frags { mm_f16x8 ah[2], al[2], bw[2]; };
+    auto load_frags = [&](const char* base, const int kk, Frags& f) {
+        const char* w_img = base;
+        const char* xh_img = base + MM_BR * C::RB;
+        const char* xl_img = base + (MM_BR + MM_BT) * C::RB;
+        const int c = 2 * kk + h;
 #pragma unroll
-        for (int kk = 0; kk < MM_BK / 16; kk++) {
-            const int c = 2 * kk + h;
-            mm_f16x8 ah[2], al[2], bw[2];
+        for (int i = 0; i < 2; i++) {
+            const uint32_t o = C::off(64 * wt + 32 * i + l32, c);
+            f.ah[i] = *(const mm_f16x8*)(xh_img + o);
+            f.al[i] = *(const mm_f16x8*)(xl_img + o);
+        }
 #pragma unroll
-            for (int i = 0; i < 2; i++) {
-                const uint32_t o = mm_lds_off(64 * wt + 32 * i + l32, c);
-                ah[i] = *(const mm_f16x8*)(xh_img + o);
-                al[i] = *(const mm_f16x8*)(xl_img + o);
+        for (int j = 0; j < 2; j++) f.bw[j] = *(const mm_f16x8*)(w_img + C::off(64 * wr + 32 * j + l32, c));
+    };
+    auto mma = [&](const Frags& f) {
+        if constexpr (FL & 2) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < 2; i++)
+#pragma unroll
+            for (int j = 0; j < 2; j++) {
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.ah[i], f.bw[j], acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.al[i], f.bw[j], acc[i][j], 0, 0, 0);
             }
+        if constexpr (FL & 2) __builtin_amdgcn_s_setprio(0);
+    };
+    auto compute = [&](const int stage) {
+        const char* base = mm_smem + stage * C::STAGE;
+        if constexpr (FL & 1) {
+            // the next 16-deep step's fragments requested before this one's MFMAs
+            Frags f0, f1;
+            load_frags(base, 0, f0);
 #pragma unroll
-            for (int j = 0; j < 2; j++) bw[j] = *(const mm_f16x8*)(wt_img + mm_lds_off(64 * wr + 32 * j + l32, c));
+            for (int kk = 0; kk < BK / 16; kk++) {
+                if (kk + 1 < BK / 16) load_frags(base, kk + 1, (kk & 1) ? f0 : f1);
+                mma((kk & 1) ? f1 : f0);
+            }
+        } else {
 #pragma unroll
-            for (int i = 0; i < 2; i++)
-#pragma unroll
-                for (int j = 0; j < 2; j++) {
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bw[j], acc[i][j], 0, 0, 0);
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bw[j], acc[i][j], 0, 0, 0);
-                }
+            for (int kk = 0; kk < BK / 16; kk++) {
+                Frags f;
+                load_frags(base, kk, f);
+                mma(f);
+            }
         }
     };
 
-    // two stages: the DMA of step kt + 1 runs under the MFMAs of step kt
-    issue(0, kbeg);
+    // ring of NS stages, NS - 1 steps of DMA ahead of the multiply
+#pragma unroll
+    for (int d = 0; d < NS - 1; d++)
+        if (d < nk) issue(d, d);
     for (int kt = 0; kt < nk; kt++) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();  // stage kt & 1 landed for every wave; stage (kt + 1) & 1 no longer read
-        if (kt + 1 < nk) issue((kt + 1) & 1, kbeg + (kt + 1) * MM_BK);
-        compute(kt & 1);
+        mm_wait_ahead<C::LPS, NS>(min(NS - 2, nk - 1 - kt));  // this wave's DMA of step kt landed
+        __builtin_amdgcn_s_barrier();                          // ... every wave's; stage kt - 1 read
+        asm volatile("" ::: "memory");
+        if (kt + NS - 1 < nk) issue((kt + NS - 1) % NS, kt + NS - 1);
+        compute(kt % NS);
     }
 
     // D: lane l holds row l & 31, tokens (reg & 3) + 8 (reg >> 2) + 4 h of each 32 x 32 tile
@@ -168,5 +250,8 @@ __global__ __launch_bounds__(MM_THREADS, 2) void mm_f16_kernel(const MmArgs a) {
             }
     }
 }
+
+// the product's instantiation
+#define mm_f16_kernel mm_f16_kernel_t<MM_BK, MM_NS, MM_FL>
 
 }  // namespace xalm

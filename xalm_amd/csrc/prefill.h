@@ -26,7 +26,7 @@
 namespace xalm {
 
 constexpr int PF_TOK = 64;       // tokens per pass of the hand-written MFMA GEMMs (two token tiles)
-constexpr int PF_TOK_MM = 1024;  // tokens per pass of the LDS-tiled f16 GEMM (gemm16.h)
+constexpr int PF_TOK_MM = 2048;  // tokens per pass of the LDS-tiled f16 GEMM (gemm16.h)
 constexpr int PF_TOK_BLAS = 512; // tokens per pass of the hipBLASLt GEMMs (XH_OPT_PREFILL 4)
 constexpr int PF_TOK_MAX = PF_TOK_MM > PF_TOK_BLAS ? PF_TOK_MM : PF_TOK_BLAS;
 constexpr int PF_THREADS = 256;  // 4 waves

@@ -824,7 +824,7 @@ bool pf_f16w(int dt) { return dt == XH_F16 || pf_f8(dt); }
 // (XH_OPT_PREFILL 1: K in whole 64-deep steps) or hipBLASLt (4: a plan for every shape)?
 bool pf_lay0(const xh_ctx* ctx, int dt, int K) {
     if (!pf_f16w(dt)) return false;
-    if (ctx->prefill_gemm == 1) return K % MM_BK == 0;
+    if (ctx->prefill_gemm == 1) return K % MM_KMULT == 0;
     if (ctx->prefill_gemm == 4) return ctx->blas_ok > 0;
     return false;
 }
@@ -952,7 +952,7 @@ int pf_gemm(xh_ctx* ctx, const char* what, int dt, const void* w, int K, int row
         }
         MmArgs a{};
         a.w = (const uint16_t*)w; a.xh = ctx->pf_xh; a.xl = ctx->pf_xh + (size_t)n * K; a.out = ctx->pf_part;
-        a.rows = rows; a.K = K; a.n = n; a.ks = mm_pick_ks(rows, K, n, 2 * ctx->pf_cap);
+        a.rows = rows; a.K = K; a.n = n; a.ks = mm_pick_ks(rows, K, n, pf_part_floats(ctx, ctx->pf_cap), ctx->n_cu);
         a.n_rt = mm_row_tiles(rows); a.n_tt = mm_tok_tiles(n);
         if (a.ks <= 0 || (size_t)a.ks * n * rows > pf_part_floats(ctx, ctx->pf_cap))
             return set_err(ctx, XH_E_INVALID, "prefill: %s GEMM %d x %d over %d tokens does not fit", what, rows, K, n);
@@ -2013,10 +2013,10 @@ int xh_op_mha(float* xout, const uint16_t* kb, const uint16_t* vb, const float* 
 
 int xh_op_prompt_gemm(float* y, const uint16_t* w, const uint16_t* xh, const uint16_t* xl, int rows, int K, int n,
                       int ks) {
-    if (!y || !w || !xh || !xl || rows <= 0 || n <= 0 || K <= 0 || K % MM_BK || ks < 0 || ks > 64)
+    if (!y || !w || !xh || !xl || rows <= 0 || n <= 0 || K <= 0 || K % MM_KMULT || ks < 0 || ks > 64)
         return set_err(nullptr, XH_E_INVALID, "bad prompt_gemm args");
-    if (ks == 0) ks = mm_pick_ks(rows, K, n, 2 * PF_TOK_MM);
-    if (K % (ks * MM_BK)) return set_err(nullptr, XH_E_INVALID, "K %d not in %d slices of 64", K, ks);
+    if (ks == 0) ks = mm_pick_ks(rows, K, n, (size_t)8 * n * rows);
+    if (ks <= 0 || K % (ks * MM_KMULT)) return set_err(nullptr, XH_E_INVALID, "K %d not in %d slices of 64", K, ks);
     DevBuf bw, bx, bo;
     int rc;
     const size_t xe = (size_t)n * K;
