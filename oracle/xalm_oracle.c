@@ -597,6 +597,39 @@ static void matmul64(double* xout, const double* x, const void* w, const int dty
         }
         return;
     }
+    if (dtype == XH_F8_E4M3 || dtype == XH_F8_E5M2 || dtype == XH_Q8) {
+        /* one-byte codes: the decode of each of the 256 codes, looked up */
+        double tab[256];
+        for (int c = 0; c < 256; c++) {
+            const uint8_t b = (uint8_t)c;
+            tab[c] = xo_decode(dtype, &b, 0);
+        }
+        const uint8_t* W = (const uint8_t*)w;
+#pragma omp parallel for schedule(static)
+        for (i = 0; i < d; i++) {
+            const uint8_t* row = W + (size_t)i * n;
+            double v0 = 0.0, v1 = 0.0;
+            int j = 0;
+            for (; j + 2 <= n; j += 2) {
+                v0 += tab[row[j]] * x[j];
+                v1 += tab[row[j + 1]] * x[j + 1];
+            }
+            for (; j < n; j++) v0 += tab[row[j]] * x[j];
+            xout[i] = v0 + v1;
+        }
+        return;
+    }
+    if (dtype == XH_BF16) {
+        const uint16_t* W = (const uint16_t*)w;
+#pragma omp parallel for schedule(static)
+        for (i = 0; i < d; i++) {
+            const uint16_t* row = W + (size_t)i * n;
+            double val = 0.0;
+            for (int j = 0; j < n; j++) val += (double)bf16_to_f32(row[j]) * x[j];
+            xout[i] = val;
+        }
+        return;
+    }
 #pragma omp parallel for schedule(static)
     for (i = 0; i < d; i++) {
         double val = 0.0;
