@@ -172,18 +172,18 @@ def test_batched_prefill_matches_oracle(name, n, mode):
     check(st.logits(), om.logits(), name, "prefill")
 
 
-@pytest.mark.parametrize("mode,n", [(1, 1200), (4, 700)])
+@pytest.mark.parametrize("mode,n", [(1, 2200), (4, 700)])
 @pytest.mark.parametrize("name", ["tiny_mistral_f16", "tiny_mistral_f8_e4m3", "small_llama_f16"])
 def test_multi_pass_prefill_matches_oracle(name, mode, n):
-    """XH_OPT_PREFILL 1 on f16 / fp8 weights: gemm16.h passes of 1024 tokens (1200 tokens = a full
-    pass and a 176-token one, the second attending over the first pass's K/V rows); 4: hipBLASLt
+    """XH_OPT_PREFILL 1 on f16 / fp8 weights: gemm16.h passes of 2048 tokens (2200 tokens = a full
+    pass and a 152-token one, the second attending over the first pass's K/V rows); 4: hipBLASLt
     passes of 512 (700 = 512 + 188).  Last logits and every layer's K/V rows vs the oracle's token
     loop, then the perplexity path over 600 tokens (lm_head as one GEMM per pass, or 64-token
     slices for bf16 lm_heads)."""
     xf = XalmFile(fixture_path(name + ".xalm"))
-    gm = Model.from_xalm(xf, context=2048)
+    gm = Model.from_xalm(xf, context=4096)
     gm.set_option(L.OPT_PREFILL, mode)
-    om = O.OracleModel.from_xalm(xf, context=2048)
+    om = O.OracleModel.from_xalm(xf, context=4096)
     toks = [1] + [3 + (i * 37) % 280 for i in range(n - 1)]
     st = InferenceState(gm.config)
     gm.prefill(toks, 0, st)
@@ -196,9 +196,9 @@ def test_multi_pass_prefill_matches_oracle(name, mode, n):
             b = om.kv(layer, which)[:n].view(np.float16).astype(np.float32)
             assert np.abs(a - b).max() <= 2e-3 * max(1.0, np.abs(b).max()), (layer, which)
     gm.close()
-    gm2 = Model.from_xalm(xf, context=2048)
+    gm2 = Model.from_xalm(xf, context=4096)
     gm2.set_option(L.OPT_PREFILL, mode)
-    om2 = O.OracleModel.from_xalm(xf, context=2048)
+    om2 = O.OracleModel.from_xalm(xf, context=4096)
     check_probs(gm2.token_probs(toks[:600]), om2, toks[:600], name)
 
 

@@ -119,11 +119,13 @@ def test_block_upload_checks():
 
 
 @pytest.mark.parametrize("name", ["tiny_mistral_q8_0", "tiny_mistral_q4_0", "small_llama_q8_0"])
-@pytest.mark.parametrize("batched", [1, 0])
+@pytest.mark.parametrize("batched", [1, 3, 0])
 def test_block_prompt_passes(name, batched):
-    """A 100-token prompt (a full 64-token pass + 36) through the batched path on gguf blocks
-    (XH_OPT_PREFILL 1) and the token loop (0) vs the oracle's HYDRATE loop: last logits, every
-    K/V row; then the perplexity path over 80 tokens (lm_head GEMM over block rows)."""
+    """A 100-token prompt through the batched path on gguf blocks (XH_OPT_PREFILL 1: the blocks'
+    exact f16 hi + lo images through gemm16.h, one pass; 3: the f32-input MFMA kernel decoding the
+    blocks in registers, a full 64-token pass + 36) and the token loop (0) vs the oracle's HYDRATE
+    loop: last logits, every K/V row; then the perplexity path over 80 tokens (lm_head GEMM over
+    block rows)."""
     xf = XalmFile(fixture_path(name + ".xalm"))
     gm = Model.from_xalm(xf, context=256)
     gm.set_option(L.OPT_PREFILL, batched)
@@ -152,3 +154,22 @@ def test_block_prompt_passes(name, batched):
             assert got[pos] < 1e-30
             continue
         check_logp(float(abs(np.log(got[pos]) - np.log(ref))), lg, name, pos)
+
+
+@pytest.mark.parametrize("name", ["tiny_mistral_q4_0", "tiny_mistral_q8_0"])
+def test_block_multi_pass_prefill(name):
+    """2200 tokens = a full 2048-token gemm16.h pass over the hi / lo block images and a 152-token
+    one attending over the first pass's K/V rows, vs the oracle's token loop."""
+    xf = XalmFile(fixture_path(name + ".xalm"))
+    gm = Model.from_xalm(xf, context=4096)
+    om = O.OracleModel.from_xalm(xf, context=4096)
+    toks = [1] + [3 + (i * 41) % (gm.config.vocab_size - 3) for i in range(2199)]
+    st = InferenceState(gm.config)
+    gm.prefill(toks, 0, st)
+    for pos, tok in enumerate(toks):
+        om.forward(tok, pos, L.OUTPUT_LOGITS if pos == len(toks) - 1 else L.HYDRATE_KV_CACHE)
+    check(st.logits(), om.logits(), name, "prefill")
+    for layer in range(gm.config.n_layers):
+        a = gm.kv_read(layer, 1, 0, len(toks)).view(np.float16).astype(np.float32)
+        b = om.kv(layer, 1)[:len(toks)].view(np.float16).astype(np.float32)
+        assert np.abs(a - b).max() <= 2e-3 * max(1.0, np.abs(b).max()), layer

@@ -777,4 +777,49 @@ __global__ __launch_bounds__(256) void pf_dequant_f16_kernel(const u32x4* w, con
     }
 }
 
+// gguf blocks (Q8_0 / Q4_0, planar device rows: codes, then one f16 scale d per 32 elements) ->
+// the exact f16 hi + lo of every weight for the f16 GEMMs of a prompt pass.  The converter's
+// value d * q (quants.py: Q8_0 :448-454, Q4_0 :302-311) is exact in f32 (11-bit d times a 4- or
+// 8-bit q) and splits exactly into hi = f16(v) and lo = f16(v - hi) (at most 19 significant bits,
+// and lo a multiple of d's ulp), so W = W_hi + W_lo with no rounding: the GEMM runs once over
+// each image.  One thread per 8 consecutive elements of a row; hi / lo: [rows][K].
+template <int DT>
+__global__ __launch_bounds__(256) void pf_dequant_gq_kernel(const uint8_t* w, const int rows, const int K,
+                                                           uint16_t* hi, uint16_t* lo) {
+    const size_t pitch = gq_pitch(DT, (size_t)K), qbytes = gq_qbytes(DT, (size_t)K);
+    const size_t per_row = (size_t)K / 8, total = (size_t)rows * per_row;
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (size_t)gridDim.x * 256) {
+        const size_t r = i / per_row;
+        const int k = (int)(i - r * per_row) * 8;  // 8 elements k .. k+7 of one block
+        const uint8_t* row = w + r * pitch;
+        const int b = k >> 5, j0 = k & 31;
+        const float d = f16_bits_to_f32(*(const uint16_t*)(row + qbytes + 2 * b));
+        int q[8];
+        if constexpr (DT == XH_Q8_0) {
+            const uint2 u = *(const uint2*)(row + k);
+#pragma unroll
+            for (int e = 0; e < 8; e++) q[e] = (int8_t)(((e < 4 ? u.x : u.y) >> (8 * (e & 3))) & 0xffu);
+        } else {
+            // element j of a block: byte j & 15 of its 16, low nibble for j < 16, high for j >= 16
+            const uint2 u = *(const uint2*)(row + 16 * b + (j0 & 15));
+#pragma unroll
+            for (int e = 0; e < 8; e++) {
+                const uint32_t byte = ((e < 4 ? u.x : u.y) >> (8 * (e & 3))) & 0xffu;
+                q[e] = (int)(j0 < 16 ? (byte & 15u) : (byte >> 4)) - 8;
+            }
+        }
+        uint32_t h[4], l[4];
+#pragma unroll
+        for (int e = 0; e < 8; e += 2) {
+            const float v0 = d * (float)q[e], v1 = d * (float)q[e + 1];
+            const _Float16 h0 = (_Float16)v0, h1 = (_Float16)v1;
+            const _Float16 l0 = (_Float16)(v0 - (float)h0), l1 = (_Float16)(v1 - (float)h1);
+            h[e / 2] = (uint32_t)__builtin_bit_cast(uint16_t, h0) | ((uint32_t)__builtin_bit_cast(uint16_t, h1) << 16);
+            l[e / 2] = (uint32_t)__builtin_bit_cast(uint16_t, l0) | ((uint32_t)__builtin_bit_cast(uint16_t, l1) << 16);
+        }
+        *(u32x4*)(hi + r * (size_t)K + k) = u32x4{h[0], h[1], h[2], h[3]};
+        *(u32x4*)(lo + r * (size_t)K + k) = u32x4{l[0], l[1], l[2], l[3]};
+    }
+}
+
 }  // namespace xalm

@@ -823,6 +823,8 @@ bool pf_f16w(int dt) { return dt == XH_F16 || pf_f8(dt); }
 // Does the GEMM over W (dtype dt, K columns) run on the row-major split input: gemm16.h
 // (XH_OPT_PREFILL 1: K in whole 64-deep steps) or hipBLASLt (4: a plan for every shape)?
 bool pf_lay0(const xh_ctx* ctx, int dt, int K) {
+    // gguf blocks: their exact f16 hi + lo images through gemm16.h (XH_OPT_PREFILL 1)
+    if (gq_dt(dt)) return ctx->prefill_gemm == 1 && K % MM_KMULT == 0;
     if (!pf_f16w(dt)) return false;
     if (ctx->prefill_gemm == 1) return K % MM_KMULT == 0;
     if (ctx->prefill_gemm == 4) return ctx->blas_ok > 0;
@@ -853,9 +855,10 @@ int pf_prepare(xh_ctx* ctx) {
         }
         ctx->blas_ok = ok;
     }
-    size_t wdq = 0;
+    size_t wdq = 0;  // fp8: one f16 image; gguf blocks: hi and lo images
     for (const G& g : gs)
-        if (pf_f8(g.dt) && pf_lay0(ctx, g.dt, g.K)) wdq = std::max(wdq, (size_t)g.rows * g.K);
+        if ((pf_f8(g.dt) || gq_dt(g.dt)) && pf_lay0(ctx, g.dt, g.K))
+            wdq = std::max(wdq, (size_t)g.rows * g.K * (gq_dt(g.dt) ? 2 : 1));
     if (wdq > ctx->pf_wdq_elems) {
         HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
         hipFree(ctx->pf_wdq);
@@ -942,6 +945,23 @@ int pf_gemm(xh_ctx* ctx, const char* what, int dt, const void* w, int K, int row
                                    (const u32x4*)w, n16, (u32x4*)ctx->pf_wdq);
             w = ctx->pf_wdq;
         }
+        const uint16_t* w_lo = nullptr;  // gguf blocks: the lo image, a second GEMM into more partials
+        if (gq_dt(dt)) {
+            if ((size_t)2 * rows * K > ctx->pf_wdq_elems || K % 32)
+                return set_err(ctx, XH_E_INVALID, "prefill: %s block image does not fit", what);
+            const size_t chunks = (size_t)rows * K / 8;
+            const int grid = (int)std::min<size_t>((chunks + 255) / 256, 8192);
+            uint16_t* hi = ctx->pf_wdq;
+            uint16_t* lo = ctx->pf_wdq + (size_t)rows * K;
+            if (dt == XH_Q8_0)
+                hipLaunchKernelGGL(pf_dequant_gq_kernel<XH_Q8_0>, dim3(grid), dim3(256), 0, ctx->stream,
+                                   (const uint8_t*)w, rows, K, hi, lo);
+            else
+                hipLaunchKernelGGL(pf_dequant_gq_kernel<XH_Q4_0>, dim3(grid), dim3(256), 0, ctx->stream,
+                                   (const uint8_t*)w, rows, K, hi, lo);
+            w = hi;
+            w_lo = lo;
+        }
         ctx->pf_scaled = true;
         if (ctx->prefill_gemm == 4) {
             // hi and lo rows as one B operand of 2n columns: partials [2][n][rows]
@@ -950,15 +970,22 @@ int pf_gemm(xh_ctx* ctx, const char* what, int dt, const void* w, int K, int row
             ks = 2;
             return 0;
         }
+        const int images = w_lo ? 2 : 1;
+        const size_t cap = pf_part_floats(ctx, ctx->pf_cap);
         MmArgs a{};
         a.w = (const uint16_t*)w; a.xh = ctx->pf_xh; a.xl = ctx->pf_xh + (size_t)n * K; a.out = ctx->pf_part;
-        a.rows = rows; a.K = K; a.n = n; a.ks = mm_pick_ks(rows, K, n, pf_part_floats(ctx, ctx->pf_cap), ctx->n_cu);
+        a.rows = rows; a.K = K; a.n = n; a.ks = mm_pick_ks(rows, K, n, cap / images, ctx->n_cu);
         a.n_rt = mm_row_tiles(rows); a.n_tt = mm_tok_tiles(n);
-        if (a.ks <= 0 || (size_t)a.ks * n * rows > pf_part_floats(ctx, ctx->pf_cap))
+        if (a.ks <= 0 || (size_t)images * a.ks * n * rows > cap)
             return set_err(ctx, XH_E_INVALID, "prefill: %s GEMM %d x %d over %d tokens does not fit", what, rows, K, n);
         ensure_lds((const void*)mm_f16_kernel, MM_LDS);
         hipLaunchKernelGGL(mm_f16_kernel, dim3(a.n_rt * a.n_tt * a.ks), dim3(MM_THREADS), MM_LDS, ctx->stream, a);
-        ks = a.ks;
+        if (w_lo) {  // partials [ks, 2 ks): W_lo . X, summed after W_hi's by the epilogue
+            a.w = w_lo;
+            a.out = ctx->pf_part + (size_t)a.ks * n * rows;
+            hipLaunchKernelGGL(mm_f16_kernel, dim3(a.n_rt * a.n_tt * a.ks), dim3(MM_THREADS), MM_LDS, ctx->stream, a);
+        }
+        ks = images * a.ks;
         return 0;
     }
     if (lay > 0) {
