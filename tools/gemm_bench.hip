@@ -11,6 +11,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <random>
 #include <vector>
 
@@ -85,13 +86,12 @@ int main(int argc, char** argv) {
     const size_t wss = 256ull << 20;
     CK(hipMalloc(&ws, wss));
     CK(hipMemcpy(dw, hw.data(), wmax * 2, hipMemcpyHostToDevice));
-    struct Var { const char* name; void (*fn)(xalm::MmArgs); int lds; };
+    struct Var { const char* name; void (*fn)(xalm::MmArgs); int lds; int bt; };
     const Var vars[] = {
-        {"bk64", xalm::mm_f16_kernel_t<64, 2, 0>, xalm::MmCfg<64, 2>::LDS},
-        {"bk64pf", xalm::mm_f16_kernel_t<64, 2, 1>, xalm::MmCfg<64, 2>::LDS},
-        {"bk64pri", xalm::mm_f16_kernel_t<64, 2, 2>, xalm::MmCfg<64, 2>::LDS},
-        {"bk64pfpr", xalm::mm_f16_kernel_t<64, 2, 3>, xalm::MmCfg<64, 2>::LDS},
-        {"bk32n4pf", xalm::mm_f16_kernel_t<32, 4, 1>, xalm::MmCfg<32, 4>::LDS},
+        {"b128", xalm::mm_f16_kernel_t<64, 2, 0, 128>, xalm::MmCfg<64, 2, 128>::LDS, 128},
+        {"b128g", xalm::mm_f16_kernel_t<64, 2, 4, 128>, xalm::MmCfg<64, 2, 128>::LDS, 128},
+        {"o4k32", xalm::mm_f16_kernel_t<32, 2, 4, 128, 4>, xalm::MmCfg<32, 2, 128>::LDS, 128},
+        {"o4k32pf", xalm::mm_f16_kernel_t<32, 2, 5, 128, 4>, xalm::MmCfg<32, 2, 128>::LDS, 128},
     };
     const int NV = sizeof vars / sizeof vars[0];
     for (int v = 0; v < NV; v++)
@@ -117,14 +117,19 @@ int main(int argc, char** argv) {
             a.w = dw; a.xh = dx; a.xl = dx + (size_t)n * sh.K; a.out = dy;
             a.rows = sh.rows; a.K = sh.K; a.n = n; a.ks = pick_ks(sh.rows, n, sh.K);
             a.n_rt = (sh.rows + xalm::MM_BR - 1) / xalm::MM_BR; a.n_tt = (n + xalm::MM_BT - 1) / xalm::MM_BT;
-            const int grid = a.n_rt * a.n_tt * a.ks;
-            const float bus = blaslt_us(bl, sh.rows, sh.K, 2 * n, dw, dx, dy, ws, wss);
+            int grid = a.n_rt * a.n_tt * a.ks;
+            if (getenv("GB_SHAPE") && strcmp(getenv("GB_SHAPE"), sh.name)) continue;
+            const float bus = getenv("GB_NOBLAS") ? 1e9f : blaslt_us(bl, sh.rows, sh.K, 2 * n, dw, dx, dy, ws, wss);
             const double flop = 2.0 * sh.rows * sh.K * (double)n;  // counted once (hi + lo = 2x MFMA work)
             tot_bl += bus;
             tot_flop += flop;
             printf("n %5d %-4s rows %5d K %5d ks %d grid %4d | hipBLASLt %8.1f us = %6.1f TF/s\n", n, sh.name, sh.rows, sh.K,
                    a.ks, grid, bus, flop / bus * 1e-6);
             for (int v = 0; v < NV; v++) {
+                if (getenv("GB_VAR") && atoi(getenv("GB_VAR")) != v) continue;
+                a.n_tt = (n + vars[v].bt - 1) / vars[v].bt;
+                a.ks = xalm::mm_pick_ks(sh.rows, sh.K, n, (size_t)2 * 2048 * 28672, 256, vars[v].bt);
+                grid = a.n_rt * a.n_tt * a.ks;
                 auto launch = [&]() {
                     hipLaunchKernelGGL(vars[v].fn, dim3(grid), dim3(xalm::MM_THREADS), vars[v].lds, 0, a);
                 };
@@ -166,8 +171,8 @@ int main(int argc, char** argv) {
                 tot_us[v] += us;
                 const bool ok = maxrel < 2e-6;
                 bad += !ok;
-                printf("    %-8s %8.1f us = %6.1f TF/s (MFMA %6.1f) err %.2e %s\n", vars[v].name, us, flop / us * 1e-6,
-                       2 * flop / us * 1e-6, maxrel, ok ? "ok" : "BAD");
+                printf("    %-8s ks %d grid %4d %8.1f us = %6.1f TF/s (MFMA %6.1f) err %.2e %s\n", vars[v].name, a.ks, grid, us,
+                       flop / us * 1e-6, 2 * flop / us * 1e-6, maxrel, ok ? "ok" : "BAD");
             }
         }
         printf("n %5d layer: hipBLASLt %8.1f us = %6.1f TF/s\n", n, tot_bl, tot_flop / tot_bl * 1e-6);

@@ -40,7 +40,7 @@ constexpr int MM_BT = 128;       // tokens per workgroup
 constexpr int MM_THREADS = 512;  // 8 waves
 constexpr int MM_BK = 64;        // k per stage of the default instantiation (mm_f16_kernel below)
 constexpr int MM_NS = 2;         // stages of the default instantiation
-constexpr int MM_FL = 0;         // flags of the default instantiation
+constexpr int MM_FL = 4;         // flags of the default instantiation: grouped tile order
 constexpr int MM_KMULT = 64;     // K (and every K slice) in whole multiples of this
 __host__ __device__ constexpr int mm_stage_bytes(const int bk) { return (MM_BR + 2 * MM_BT) * bk * 2; }
 constexpr int MM_LDS = MM_NS * mm_stage_bytes(MM_BK);
@@ -58,7 +58,7 @@ struct MmArgs {
 };
 
 __host__ __device__ constexpr int mm_row_tiles(const int rows) { return (rows + MM_BR - 1) / MM_BR; }
-__host__ __device__ constexpr int mm_tok_tiles(const int n) { return (n + MM_BT - 1) / MM_BT; }
+__host__ __device__ constexpr int mm_tok_tiles(const int n, const int bt = MM_BT) { return (n + bt - 1) / bt; }
 // K slices (1, 2, 4, 8): minimise the modelled time rounds(ks) * (1 / ks + MM_WG_FIXED), rounds =
 // ceil(tiles * ks / n_cu) (workgroups over the CUs) and MM_WG_FIXED a workgroup's fixed cost
 // (prologue, partial stores, tail) in units of one full-K tile, fitted to tools/gemm_bench on
@@ -66,9 +66,10 @@ __host__ __device__ constexpr int mm_tok_tiles(const int n) { return (n + MM_BT 
 // W1/W3 at 512 tokens split 4-way +14 %); K in whole 64-deep steps per slice and
 // ks * n * rows <= max_floats (the partials buffer); 0 if K is not a multiple of 64
 constexpr double MM_WG_FIXED = 0.15;
-inline int mm_pick_ks(const int rows, const int K, const int n, const size_t max_floats, const int n_cu = 256) {
+inline int mm_pick_ks(const int rows, const int K, const int n, const size_t max_floats, const int n_cu = 256,
+                      const int bt = MM_BT) {
     if (K % MM_KMULT) return 0;
-    const int tiles = mm_row_tiles(rows) * mm_tok_tiles(n);
+    const int tiles = mm_row_tiles(rows) * mm_tok_tiles(n, bt);
     int best = 1;
     double best_t = 1e30;
     for (int ks = 1; ks <= 8; ks *= 2) {
@@ -89,18 +90,22 @@ __device__ __forceinline__ void mm_wait_vm() {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <int BK, int NS>
+template <int BK, int NS, int BT = 128>
 struct MmCfg {
     static constexpr int RB = BK * 2;             // LDS image row bytes
     static constexpr int CH = RB / 16;            // 16-B chunks per row
     static constexpr int RPI = 1024 / RB;         // image rows per DMA wave-instruction
     static constexpr int SH = CH == 8 ? 1 : 2;    // swizzle f(r) = (r >> SH) & (CH - 1)
-    static constexpr int STAGE = mm_stage_bytes(BK);
+    static constexpr int STAGE = (MM_BR + 2 * BT) * RB;
     static constexpr int WI = MM_BR / RPI / 8;    // W instructions per wave per stage
-    static constexpr int XI = MM_BT / RPI / 8;    // Xh (and Xl) instructions per wave per stage
+    static constexpr int XI = BT / RPI / 8;       // Xh (and Xl) instructions per wave per stage
     static constexpr int LPS = WI + 2 * XI;       // DMA instructions per wave per stage
     static constexpr int LDS = NS * STAGE;
+    static constexpr int WT = BT / 64;            // waves along the tokens (64 tokens each)
+    static constexpr int WR = 8 / WT;             // waves along the rows
+    static constexpr int RT = MM_BR / WR / 32;    // 32-row tiles per wave
     static_assert(BK == 32 || BK == 64, "BK");
+    static_assert(BT == 128 || BT == 256, "BT");
     static_assert(NS >= 2 && LDS <= 160 * 1024, "stages");
     __device__ static uint32_t off(const int r, const int c) { return (uint32_t)(r * RB + 16 * (c ^ ((r >> SH) & (CH - 1)))); }
 };
@@ -115,10 +120,13 @@ __device__ __forceinline__ void mm_wait_ahead(const int ahead) {
 }
 
 // FL bit 0: a k-step's next fragments read before its current MFMAs; bit 1: s_setprio(1) around
-// the MFMA clusters
-template <int BK, int NS, int FL>
-__global__ __launch_bounds__(MM_THREADS, 2) void mm_f16_kernel_t(const MmArgs a) {
-    using C = MmCfg<BK, NS>;
+// the MFMA clusters; bit 2: grouped tile order (8 row tiles x n_tt token tiles per group, row tile
+// fastest: the 32 workgroups an XCD runs at once cover 8 x 4 tiles, sharing both operands in L2)
+// OCC: waves per SIMD the register allocation must allow (2: one 512-thread workgroup per CU;
+// 4: two, each with at most 80 KiB of LDS)
+template <int BK, int NS, int FL, int BT = 128, int OCC = 2>
+__global__ __launch_bounds__(MM_THREADS, OCC) void mm_f16_kernel_t(const MmArgs a) {
+    using C = MmCfg<BK, NS, BT>;
     extern __shared__ __attribute__((aligned(16))) char mm_smem[];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int h = lane >> 5, l32 = lane & 31;
@@ -126,9 +134,20 @@ __global__ __launch_bounds__(MM_THREADS, 2) void mm_f16_kernel_t(const MmArgs a)
     const int nb = gridDim.x, b = blockIdx.x;
     const int q = nb >> 3, rem = nb & 7, xcd = b & 7;
     const int L = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + (b >> 3);
-    const int tt = L % a.n_tt, rest = L / a.n_tt;
-    const int s = rest % a.ks, rt = rest / a.ks;
-    const int row0 = rt * MM_BR, t0 = tt * MM_BT;
+    int tt, R;  // token tile, row tile x slice (R = rt * ks + s)
+    if constexpr (FL & 4) {
+        constexpr int GR = 8;
+        const int n_R = a.n_rt * a.ks, per_group = GR * a.n_tt;
+        const int grp = L / per_group, in = L - grp * per_group;
+        const int gr = min(n_R - grp * GR, GR);
+        R = grp * GR + in % gr;
+        tt = in / gr;
+    } else {
+        tt = L % a.n_tt;
+        R = L / a.n_tt;
+    }
+    const int s = R % a.ks, rt = R / a.ks;
+    const int row0 = rt * MM_BR, t0 = tt * BT;
     const int kslice = a.K / a.ks, kbeg = s * kslice, nk = kslice / BK;
     const size_t K = (size_t)a.K;
 
@@ -166,21 +185,22 @@ __global__ __launch_bounds__(MM_THREADS, 2) void mm_f16_kernel_t(const MmArgs a)
 #pragma unroll
         for (int i = 0; i < C::XI; i++)
             __builtin_amdgcn_global_load_lds((const void*)(lsrc[i] + k),
-                                             (mm_lds_ptr)(base + (MM_BR + MM_BT) * C::RB + (wv * C::XI + i) * 1024), 16,
+                                             (mm_lds_ptr)(base + (MM_BR + BT) * C::RB + (wv * C::XI + i) * 1024), 16,
                                              0, 0);
     };
 
-    const int wt = wv >> 2, wr = wv & 3;  // this wave's 64 tokens / 64 rows of the tile
-    mm_f32x16 acc[2][2];
+    constexpr int RT = C::RT;
+    const int wt = wv / C::WR, wr = wv % C::WR;  // this wave's 64 tokens / RT x 32 rows of the tile
+    mm_f32x16 acc[2][RT];
 #pragma unroll
     for (int i = 0; i < 2; i++)
 #pragma unroll
-        for (int j = 0; j < 2; j++) acc[i][j] = mm_f32x16{};
-    struct Frags { mm_f16x8 ah[2], al[2], bw[2]; };
+        for (int j = 0; j < RT; j++) acc[i][j] = mm_f32x16{};
+    struct Frags { mm_f16x8 ah[2], al[2], bw[RT]; };
     auto load_frags = [&](const char* base, const int kk, Frags& f) {
         const char* w_img = base;
         const char* xh_img = base + MM_BR * C::RB;
-        const char* xl_img = base + (MM_BR + MM_BT) * C::RB;
+        const char* xl_img = base + (MM_BR + BT) * C::RB;
         const int c = 2 * kk + h;
 #pragma unroll
         for (int i = 0; i < 2; i++) {
@@ -189,14 +209,14 @@ __global__ __launch_bounds__(MM_THREADS, 2) void mm_f16_kernel_t(const MmArgs a)
             f.al[i] = *(const mm_f16x8*)(xl_img + o);
         }
 #pragma unroll
-        for (int j = 0; j < 2; j++) f.bw[j] = *(const mm_f16x8*)(w_img + C::off(64 * wr + 32 * j + l32, c));
+        for (int j = 0; j < RT; j++) f.bw[j] = *(const mm_f16x8*)(w_img + C::off(32 * RT * wr + 32 * j + l32, c));
     };
     auto mma = [&](const Frags& f) {
         if constexpr (FL & 2) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int i = 0; i < 2; i++)
 #pragma unroll
-            for (int j = 0; j < 2; j++) {
+            for (int j = 0; j < RT; j++) {
                 acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.ah[i], f.bw[j], acc[i][j], 0, 0, 0);
                 acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.al[i], f.bw[j], acc[i][j], 0, 0, 0);
             }
@@ -238,8 +258,8 @@ __global__ __launch_bounds__(MM_THREADS, 2) void mm_f16_kernel_t(const MmArgs a)
     // D: lane l holds row l & 31, tokens (reg & 3) + 8 (reg >> 2) + 4 h of each 32 x 32 tile
     float* out = a.out + (size_t)s * a.n * a.rows;
 #pragma unroll
-    for (int j = 0; j < 2; j++) {
-        const int r = row0 + 64 * wr + 32 * j + l32;
+    for (int j = 0; j < RT; j++) {
+        const int r = row0 + 32 * RT * wr + 32 * j + l32;
         if (r >= a.rows) continue;
 #pragma unroll
         for (int i = 0; i < 2; i++)
@@ -252,6 +272,6 @@ __global__ __launch_bounds__(MM_THREADS, 2) void mm_f16_kernel_t(const MmArgs a)
 }
 
 // the product's instantiation
-#define mm_f16_kernel mm_f16_kernel_t<MM_BK, MM_NS, MM_FL>
+#define mm_f16_kernel mm_f16_kernel_t<MM_BK, MM_NS, MM_FL, MM_BT>
 
 }  // namespace xalm
