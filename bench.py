@@ -429,14 +429,15 @@ def main():
         flops = 2.0 * args.prefill_tokens * c.n_layers * layer_params  # matrix products only
         prefill = {"tokens": args.prefill_tokens, "ms": round(pf_s * 1e3, 2),
                    "tok_s": round(args.prefill_tokens / pf_s, 1),
-                   "mode": {0: "per-token", 1: "batched: gemm16.h LDS-tiled f16 MFMA GEMM (f16 / fp8 weights), "
-                                               "else register-streaming MFMA kernels",
+                   "mode": {0: "per-token", 1: "batched: gemm16.h LDS-tiled f16 MFMA GEMM (f16 / fp8 / gguf-block "
+                                               "weights), else register-streaming MFMA kernels",
                             2: "batched split-f16 register-streaming MFMA", 3: "batched f32-input MFMA",
                             4: "batched: hipBLASLt f16 GEMMs (f16 / fp8 weights)"}[model.get_option(L.OPT_PREFILL)],
-                   "note": "f16 / fp8 weights: passes of up to 1024 tokens (hipBLASLt: 512), f16 GEMMs (fp8 matrices "
-                           "through their exact f16 image) over f16 hi+lo activation pairs (power-of-two row scale, "
-                           "~22-bit mantissa), hi and lo accumulated in f32; other dtypes (bf16, gguf blocks): passes "
-                           "of 64 tokens on the register-streaming MFMA GEMMs (f32 activations as the reference)",
+                   "note": "f16 / fp8 / gguf-block weights: passes of up to 2048 tokens (hipBLASLt: 512), f16 GEMMs "
+                           "(fp8 matrices through their exact f16 image, gguf blocks through exact f16 hi + lo images) "
+                           "over f16 hi+lo activation pairs (power-of-two row scale, ~22-bit mantissa), hi and lo "
+                           "accumulated in f32; other dtypes (bf16, f32, Q8): passes of 64 tokens on the f32-input "
+                           "MFMA GEMM (f32 activations as the reference)",
                    "matmul_tflops": round(flops / pf_s / 1e12, 1)}
         # run_perplexity's loop (xh_perplexity): the same tokens, every token's logits and
         # sample_prob of the next one on the device

@@ -88,10 +88,9 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(dw, hw.data(), wmax * 2, hipMemcpyHostToDevice));
     struct Var { const char* name; void (*fn)(xalm::MmArgs); int lds; int bt; };
     const Var vars[] = {
-        {"b128", xalm::mm_f16_kernel_t<64, 2, 0, 128>, xalm::MmCfg<64, 2, 128>::LDS, 128},
         {"b128g", xalm::mm_f16_kernel_t<64, 2, 4, 128>, xalm::MmCfg<64, 2, 128>::LDS, 128},
-        {"o4k32", xalm::mm_f16_kernel_t<32, 2, 4, 128, 4>, xalm::MmCfg<32, 2, 128>::LDS, 128},
-        {"o4k32pf", xalm::mm_f16_kernel_t<32, 2, 5, 128, 4>, xalm::MmCfg<32, 2, 128>::LDS, 128},
+        {"m16g", xalm::mm_f16_kernel_t<64, 2, 12, 128>, xalm::MmCfg<64, 2, 128>::LDS, 128},
+        {"m16gpr", xalm::mm_f16_kernel_t<64, 2, 14, 128>, xalm::MmCfg<64, 2, 128>::LDS, 128},
     };
     const int NV = sizeof vars / sizeof vars[0];
     for (int v = 0; v < NV; v++)
