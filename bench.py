@@ -450,21 +450,22 @@ def main():
                                  "finite": bool(np.isfinite(np.log(probs)).all())}
 
     # configs[3]: a prompt pass over a long history (the MFMA prompt attention walks slots
-    # [0, pos] per wave; XH_OPT_PREFILL_ATTN 0 = the split-KV per-token attention), timed at the
+    # [0, pos] per workgroup (1) or per wave (2); XH_OPT_PREFILL_ATTN 0 = the split-KV per-token
+    # attention), timed at the
     # end of the 32k ring
     if args.prefill_tokens and w["kv_prefill"] and args.prefill_tokens < c.max_seq_len:
         ptoks = prompt_tokens(c.vocab_size, n=args.prefill_tokens, seed=11)
         p0 = c.max_seq_len - args.prefill_tokens - 1
         model.set_option(L.OPT_PREFILL, args.prefill_mode)
         res = {}
-        for attn in (1, 0):
+        for attn, name in ((1, "mfma_shared_tiles"), (2, "mfma_per_wave_tiles"), (0, "split_kv")):
             model.set_option(L.OPT_PREFILL_ATTN, attn)
             model.prefill(ptoks, p0, st)  # warm
             sync_all(None, torch_mod)
             t0 = time.perf_counter()
             model.prefill(ptoks, p0, st)
             sync_all(None, torch_mod)
-            res["mfma_tiles" if attn else "split_kv"] = round(args.prefill_tokens / (time.perf_counter() - t0), 1)
+            res[name] = round(args.prefill_tokens / (time.perf_counter() - t0), 1)
         model.set_option(L.OPT_PREFILL_ATTN, 1)
         prefill = {"tokens": args.prefill_tokens, "pos0": p0, "tok_s_by_attention": res,
                    "note": "prompt pass at the end of the -T 32768 ring: each token attends over ~30k slots"}

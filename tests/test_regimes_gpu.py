@@ -349,12 +349,12 @@ def test_launch_structures_match_oracle(wdt, history, fuse):
 # algorithm: tests/test_parity_full_gpu.py)
 
 
-@pytest.mark.parametrize("attn", [1, 0])
+@pytest.mark.parametrize("attn", [1, 2, 0])
 @pytest.mark.parametrize("heads,kv_heads,head_dim,wdt", [(8, 2, 128, L.F16), (16, 2, 128, L.F16),
                                                           (8, 2, 64, L.F8_E4M3), (4, 2, 16, L.BF16)])
 def test_prompt_attention_in_two_prompts(heads, kv_heads, head_dim, wdt, attn):
-    """xh_prefill's causal attention (XH_OPT_PREFILL_ATTN 1: MFMA tiles; 0: per-token split
-    kernel) at every instantiated head shape (QPK 4 / 8 / 2, head_dim 128 / 64 / 16), a prompt
+    """xh_prefill's causal attention (XH_OPT_PREFILL_ATTN 1: MFMA tiles shared by a workgroup's
+    waves; 2: per-wave MFMA tiles; 0: per-token split kernel) at every instantiated head shape (QPK 4 / 8 / 2, head_dim 128 / 64 / 16), a prompt
     of 600 tokens followed by a second prompt of 300 at pos 600 (its rows attend over the first
     prompt's K/V), against the oracle's token loop: last logits and every K/V row.  f16
     weights run 512-token passes (attention over a pass boundary), bf16 64-token ones."""
@@ -376,3 +376,28 @@ def test_prompt_attention_in_two_prompts(heads, kv_heads, head_dim, wdt, attn):
             a = f16(gm.kv_read(layer, which, 0, len(toks)))
             b = f16(om.kv(layer, which)[:len(toks)])
             assert np.abs(a - b).max() <= 2e-3 * max(1.0, np.abs(b).max()), (layer, which)
+
+
+@pytest.mark.parametrize("heads,kv_heads", [(8, 2), (16, 2)])
+def test_prompt_attention_shared_tiles_bit_identical(heads, kv_heads):
+    """XH_OPT_PREFILL_ATTN 1 (K/V tiles DMA'd once per workgroup, ring in LDS, V read by
+    transposed LDS reads) runs prefill_fa_kernel's per-wave arithmetic unchanged: logits and
+    every K/V row of ragged prompts (a 333-token prompt, then 1000 tokens at pos 333, a pass
+    boundary at 2048 crossed by 37 + 1400 more) are bit-identical to XH_OPT_PREFILL_ATTN 2."""
+    c = make_cfg(256, 512, 2, heads, kv_heads, 128, 512, 4096)
+    toks = [1] + [3 + (i * 53) % 500 for i in range(2769)]
+    cuts = [0, 333, 1333, 2770]
+    res = []
+    for attn in (1, 2):
+        gm, om = build_pair(c, L.F16)
+        om.close()
+        gm.set_option(L.OPT_PREFILL_ATTN, attn)
+        st = InferenceState(c)
+        for a, b in zip(cuts[:-1], cuts[1:]):
+            gm.prefill(toks[a:b], a, st)
+        kv = [gm.kv_read(layer, which, 0, len(toks)) for layer in range(c.n_layers) for which in (0, 1)]
+        res.append((st.logits().copy(), kv))
+        gm.close()
+    assert np.array_equal(res[0][0], res[1][0])
+    for a, b in zip(res[0][1], res[1][1]):
+        assert np.array_equal(a, b)

@@ -41,7 +41,8 @@ __global__ __launch_bounds__(THREADS) void k_signal(const AttnArgs a, unsigned* 
 // diagnostic floor: the split's K rows then V rows (same per-thread addresses as attn_block:
 // 16 lanes per 256-B row slice, ATTN_PREF rows per thread per round) with D rounds in flight,
 // nothing computed but an xor (the memory side of the round loop alone)
-template <int THREADS, int D>
+// HM: head-major ring ([g][slot][HD], 32768 slots per head) instead of [slot][kv_dim]
+template <int THREADS, int D, bool HM = false>
 __global__ __launch_bounds__(THREADS) void k_stream(const AttnArgs a, unsigned* sink) {
     constexpr int LPR = HD / 8, RPP = THREADS / LPR, STEP = ATTN_PREF * RPP;
     const int g = blockIdx.x / a.nsplit, s = blockIdx.x % a.nsplit;
@@ -50,7 +51,8 @@ __global__ __launch_bounds__(THREADS) void k_stream(const AttnArgs a, unsigned* 
     const int t0 = s * T, t1 = min(kv_len, t0 + T);
     if (t0 >= kv_len) return;
     const int sub = threadIdx.x % LPR, rr = threadIdx.x / LPR;
-    const size_t col = (size_t)g * HD + sub * 8;
+    const size_t col = HM ? (size_t)g * 32768 * HD + sub * 8 : (size_t)g * HD + sub * 8;
+    const size_t pitch = HM ? HD : a.kv_dim;
     uint32_t acc = 0;
     for (int pass = 0; pass < 2; pass++) {
         const uint16_t* base = pass ? a.vc : a.kc;
@@ -60,7 +62,7 @@ __global__ __launch_bounds__(THREADS) void k_stream(const AttnArgs a, unsigned* 
         for (int d = 0; d < D; d++)
 #pragma unroll
             for (int p = 0; p < ATTN_PREF; p++)
-                r[d][p] = __builtin_nontemporal_load((const u32x4*)(base + (size_t)min(t0 + d * STEP + rr + p * RPP, t1 - 1) * a.kv_dim + col));
+                r[d][p] = __builtin_nontemporal_load((const u32x4*)(base + (size_t)min(t0 + d * STEP + rr + p * RPP, t1 - 1) * pitch + col));
         for (int k = 0; k < nr; k += D) {
 #pragma unroll
             for (int d = 0; d < D; d++) {
@@ -68,7 +70,7 @@ __global__ __launch_bounds__(THREADS) void k_stream(const AttnArgs a, unsigned* 
                 for (int p = 0; p < ATTN_PREF; p++) acc ^= r[d][p].x ^ r[d][p].w;
 #pragma unroll
                 for (int p = 0; p < ATTN_PREF; p++)
-                    r[d][p] = __builtin_nontemporal_load((const u32x4*)(base + (size_t)min(t0 + (k + d + D) * STEP + rr + p * RPP, t1 - 1) * a.kv_dim + col));
+                    r[d][p] = __builtin_nontemporal_load((const u32x4*)(base + (size_t)min(t0 + (k + d + D) * STEP + rr + p * RPP, t1 - 1) * pitch + col));
             }
         }
     }
@@ -137,6 +139,8 @@ int main(int argc, char** argv) {
         run(k_stream<1024, 2>, 1024, ns, 0, "stream  t1024 D2");
         run(k_stream<1024, 3>, 1024, ns, 0, "stream  t1024 D3");
         run(k_stream<1024, 4>, 1024, ns, 0, "stream  t1024 D4");
+        run(k_stream<1024, 2, true>, 1024, ns, 0, "stream HM t1024 D2");
+        run(k_stream<1024, 3, true>, 1024, ns, 0, "stream HM t1024 D3");
         run(k_round<1024>, 1024, ns, attn_smem_bytes(HD, QPK, T, ns, 1024), "round   t1024");
     }
     for (int ns : {32, 64, 128}) {

@@ -4,7 +4,7 @@
 # Each GPU step has its own limit; a crash / abort / timeout ends the run.
 set -u
 cd "$(dirname "$0")/.."
-ROUND=${ROUND:-r03}
+ROUND=${ROUND:-r04}
 PART=${PART:-all}   # a: tests, PMC, kernel trace, fp16 / fp8 benches; b: the other workloads
 OUT=gpurun_out/$ROUND
 mkdir -p "$OUT"
@@ -33,6 +33,12 @@ cp "$OUT/pmc.json" "profiles/${ROUND}_pmc.json"   # read by bench.py's roofline.
 step kernel_trace 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
     python3 bench.py --steps 64 --warmup 4 --no-cpu-baseline --kernel-iters 50 --prefill-tokens 0
 cp "$OUT/prof/run_kernel_stats.csv" "$OUT/kernel_stats.csv"
+step kernel_trace_f8 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_f8" -o run --output-format csv -- \
+    python3 bench.py --workload mistral-7b-f8 --steps 64 --warmup 4 --no-cpu-baseline --kernel-iters 50 --prefill-tokens 0
+cp "$OUT/prof_f8/run_kernel_stats.csv" "$OUT/kernel_stats_f8.csv"
+step kernel_trace_prefill 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_pf" -o run --output-format csv -- \
+    python3 bench.py --steps 4 --warmup 1 --no-cpu-baseline --kernel-iters 5 --prefill-tokens 2048
+cp "$OUT/prof_pf/run_kernel_stats.csv" "$OUT/kernel_stats_prefill.csv"
 step bench 600 python3 bench.py
 step bench_f8 600 python3 bench.py --workload mistral-7b-f8
 fi

@@ -21,6 +21,7 @@
 #pragma once
 
 #include "attention.h"
+#include "gemm16.h"
 #include "gemv.h"
 
 namespace xalm {
@@ -756,6 +757,194 @@ __global__ __launch_bounds__(64) void prefill_fa_kernel(const float* q, const ui
             if (d < HD)
                 *(float4*)(orow + d) =
                     float4{o[dt][r] * inv_l, o[dt][r + 1] * inv_l, o[dt][r + 2] * inv_l, o[dt][r + 3] * inv_l};
+        }
+}
+
+// ---- the same causal attention with K/V tiles shared by NW waves (head_dim 128) -------------
+// prefill_fa_kernel's per-wave arithmetic, unchanged (same tiles, same MFMA order: the outputs
+// are bit-identical), but a workgroup of NW waves covers NW x 32 query rows of one KV head and
+// each 32-slot K / V tile goes L2 -> LDS ONCE for all of them, by global_load_lds_dwordx4, into a
+// ring of FA_NS stages issued FA_NS - 1 tiles ahead of the multiply (counted vmcnt + raw
+// s_barrier, as gemm16.h).  The single-wave kernel reads every K / V row once per wave from L2
+// with its loads exposed (one round trip per tile); here a tile costs one DMA per NW waves and
+// its latency hides under the previous tiles' MFMAs.
+// LDS image of a tile ([32 slots][128 f16], 256-B rows): 16-B chunk c of row r at byte
+// 256 r + 16 (c ^ (((r & 3) << 2) | ((r >> 2) & 3))) — one image serves the K row reads (S^T's
+// A operand, ds_read_b128) and the V column reads (O^T's A operand = V^T, ds_read_b64_tr_b16:
+// lane 4q+p of a 16-lane group gives row q, columns 4p..4p+3 of a 4 x 16 block and receives
+// column (lane & 15) of the 4 rows), both conflict-free.  DMA writes are lane-linear, so the
+// chunk permutation is applied to the per-lane source address.  Slots past the workgroup's last
+// are clamped to it (valid rows; their p is 0 in every wave).
+constexpr int FA_NS = 3;                 // ring stages
+#ifndef PF_FA_WAVES
+#define PF_FA_WAVES 4                    // waves per workgroup
+#endif
+constexpr int FA_TILE_BYTES = 32 * 256;  // one K (or V) tile at head_dim 128
+__host__ __device__ constexpr int fa_lds_bytes() { return FA_NS * 2 * FA_TILE_BYTES; }
+__device__ __forceinline__ uint32_t fa_off(const int r, const int c) {
+    return (uint32_t)(256 * r + 16 * (c ^ (((r & 3) << 2) | ((r >> 2) & 3))));
+}
+typedef short fa_s16x4 __attribute__((ext_vector_type(4)));
+
+template <int QPK, int NW>
+__global__ __launch_bounds__(64 * NW, 2) void prefill_fa2_kernel(const float* q, const uint16_t* kc, const uint16_t* vc,
+                                                               float* out, int n, int pos0, int q_stride, int kv_dim) {
+    constexpr int HD = 128;
+    constexpr int TPW = 32 / QPK;        // tokens per wave
+    constexpr int KS = HD / 16;          // k steps of q . k
+    constexpr int NDT = HD / 32;         // 32-row d tiles of O^T
+    constexpr int IPW = 16 / NW;         // DMA wave-instructions per wave per stage (16 x 1 KiB)
+    static_assert(32 % QPK == 0 && 16 % NW == 0, "prefill_fa2_kernel: shape");
+    extern __shared__ __attribute__((aligned(16))) char fa_smem[];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int j32 = lane & 31, h = lane >> 5;
+    const int g = blockIdx.x;
+    const int tb = (gridDim.y - 1 - blockIdx.y) * (NW * TPW);  // longest rows first
+    const int t0 = tb + wv * TPW;                              // this wave's first token
+    const int tq = t0 + j32 / QPK;
+    const int tqc = min(tq, n - 1);
+    const int pos = pos0 + tqc;
+    const int head = g * QPK + j32 % QPK;
+    const int last = t0 < n ? pos0 + min(t0 + TPW, n) - 1 : -1;  // this wave's last slot (-1: no rows)
+    const int last_wg = pos0 + min(tb + NW * TPW, n) - 1;   // the workgroup's
+    const float scale = 1.0f / sqrtf((float)HD);  // src/infer.cpp:338
+
+    // DMA sources: instruction i of this wave = image (i >> 3: K, V), rows 4 (i & 7) .. + 3
+    int drow[IPW], dch[IPW];
+#pragma unroll
+    for (int k = 0; k < IPW; k++) {
+        const int i = wv * IPW + k;
+        drow[k] = 4 * (i & 7) + (lane >> 4);
+        dch[k] = (lane & 15) ^ (((drow[k] & 3) << 2) | ((drow[k] >> 2) & 3));
+    }
+    const int ntile = last_wg / 32 + 1;
+    auto issue = [&](const int stage, const int tile) {
+        char* base = fa_smem + stage * 2 * FA_TILE_BYTES;
+#pragma unroll
+        for (int k = 0; k < IPW; k++) {
+            const int i = wv * IPW + k;
+            const uint16_t* src = (i < 8 ? kc : vc) + (size_t)min(32 * tile + drow[k], last_wg) * kv_dim +
+                                  (size_t)g * HD + 8 * dch[k];
+            __builtin_amdgcn_global_load_lds((const void*)src,
+                                             (__attribute__((address_space(3))) void*)(base + i * 1024), 16, 0, 0);
+        }
+    };
+    // q row, split: this lane's k = 16 ks + 8 h + e (loads before the ring's first DMA)
+    f16x8 qh[KS], ql[KS];
+    float inv_s;
+    {
+        const float* qr = q + (size_t)tqc * q_stride + (size_t)head * HD;
+        float v[KS][8];
+#pragma unroll
+        for (int ks = 0; ks < KS; ks++) {
+            const float4 a = *(const float4*)(qr + 16 * ks + 8 * h), b = *(const float4*)(qr + 16 * ks + 8 * h + 4);
+            v[ks][0] = a.x; v[ks][1] = a.y; v[ks][2] = a.z; v[ks][3] = a.w;
+            v[ks][4] = b.x; v[ks][5] = b.y; v[ks][6] = b.z; v[ks][7] = b.w;
+        }
+        float mx = 0.f;
+#pragma unroll
+        for (int ks = 0; ks < KS; ks++)
+#pragma unroll
+            for (int e = 0; e < 8; e++) mx = fmaxf(mx, fabsf(v[ks][e]));
+        mx = fmaxf(mx, __shfl_xor(mx, 32));
+        int ex = 0;
+        const bool ok = mx > 0.f && mx <= FLT_MAX;
+        if (ok) frexpf(mx, &ex);
+        const float sc = ok ? ldexpf(1.f, 15 - ex) : 1.f;
+        inv_s = 1.f / sc;
+#pragma unroll
+        for (int ks = 0; ks < KS; ks++)
+#pragma unroll
+            for (int e = 0; e < 8; e++) {
+                const float u = v[ks][e] * sc;
+                qh[ks][e] = (_Float16)u;
+                ql[ks][e] = (_Float16)(u - (float)qh[ks][e]);
+            }
+    }
+    mm_wait_vm<0>();
+#pragma unroll
+    for (int d = 0; d < FA_NS - 1; d++)
+        if (d < ntile) issue(d, d);
+
+    f32x16 o[NDT];
+#pragma unroll
+    for (int dt = 0; dt < NDT; dt++) o[dt] = f32x16{};
+    float m = -INFINITY, lsum = 0.f;
+    // tr-read addresses of this lane inside a V image (block rows r0 + q, d columns of dt)
+    const int grp = lane >> 4, qq = (lane >> 2) & 3, pp = lane & 3;
+    for (int kt = 0; kt < ntile; kt++) {
+        mm_wait_ahead<IPW, FA_NS>(min(FA_NS - 2, ntile - 1 - kt));  // this wave's DMA of tile kt landed
+        __builtin_amdgcn_s_barrier();                                // ... every wave's; tile kt - 1 read
+        asm volatile("" ::: "memory");
+        if (kt + FA_NS - 1 < ntile) issue((kt + FA_NS - 1) % FA_NS, kt + FA_NS - 1);
+        const int b = 32 * kt;
+        if (b > last) continue;  // wave-uniform: past this wave's rows (it still issues its DMA share)
+        const char* kimg = fa_smem + (kt % FA_NS) * 2 * FA_TILE_BYTES;
+        const char* vimg = kimg + FA_TILE_BYTES;
+        // S^T = K Q^T
+        f32x16 st = f32x16{};
+#pragma unroll
+        for (int ks = 0; ks < KS; ks++) {
+            const f16x8 kf = *(const f16x8*)(kimg + fa_off(j32, 2 * ks + h));
+            st = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf, qh[ks], st, 0, 0, 0);
+            st = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf, ql[ks], st, 0, 0, 0);
+        }
+        // online softmax over this lane's 16 slots and its partner's (as prefill_fa_kernel)
+        float sv[16];
+        float tm = -INFINITY;
+#pragma unroll
+        for (int r = 0; r < 16; r++) {
+            const int slot = b + (r & 3) + 8 * (r >> 2) + 4 * h;
+            sv[r] = slot <= pos ? st[r] * inv_s * scale : -INFINITY;
+            tm = fmaxf(tm, sv[r]);
+        }
+        tm = fmaxf(tm, __shfl_xor(tm, 32));
+        const float mn = fmaxf(m, tm);  // finite: slot 0 <= pos on the first tile
+        const float alpha = expf(m - mn);
+        m = mn;
+        float ps = 0.f;
+        f16x8 ph[2], pl[2];
+#pragma unroll
+        for (int r = 0; r < 16; r++) {
+            const float p = expf(sv[r] - mn);
+            ps += p;
+            const _Float16 hi = (_Float16)p;
+            ph[r >> 3][r & 7] = hi;
+            pl[r >> 3][r & 7] = (_Float16)(p - (float)hi);
+        }
+        lsum = lsum * alpha + ps;
+#pragma unroll
+        for (int dt = 0; dt < NDT; dt++) o[dt] *= alpha;
+        // O^T += V^T P^T: element e of the A fragment = slot 16 s2 + 8 (e >> 2) + 4 h + (e & 3)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; s2++) {
+#pragma unroll
+            for (int dt = 0; dt < NDT; dt++) {
+                const int r0 = 16 * s2 + 4 * h + qq, c0 = 4 * dt + 2 * (grp & 1) + (pp >> 1);
+                typedef __attribute__((address_space(3))) fa_s16x4 lds_s16x4;
+                const fa_s16x4 x0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                    (lds_s16x4*)(vimg + fa_off(r0, c0) + 8 * (pp & 1)));
+                const fa_s16x4 x1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                    (lds_s16x4*)(vimg + fa_off(r0 + 8, c0) + 8 * (pp & 1)));
+                typedef short s16x8 __attribute__((ext_vector_type(8)));
+                const s16x8 xv = __builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7);
+                const f16x8 vv = __builtin_bit_cast(f16x8, xv);
+                o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vv, ph[s2], o[dt], 0, 0, 0);
+                o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vv, pl[s2], o[dt], 0, 0, 0);
+            }
+        }
+    }
+    const float l = lsum + __shfl_xor(lsum, 32);
+    if (tq >= n) return;
+    const float inv_l = 1.f / l;
+    float* orow = out + (size_t)tq * q_stride + (size_t)head * HD;
+#pragma unroll
+    for (int dt = 0; dt < NDT; dt++)
+#pragma unroll
+        for (int r = 0; r < 16; r += 4) {
+            const int d = 32 * dt + 8 * (r >> 2) + 4 * h;
+            *(float4*)(orow + d) =
+                float4{o[dt][r] * inv_l, o[dt][r + 1] * inv_l, o[dt][r + 2] * inv_l, o[dt][r + 3] * inv_l};
         }
 }
 

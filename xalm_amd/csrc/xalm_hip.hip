@@ -147,7 +147,8 @@ struct xh_ctx {
     size_t pf_wdq_elems = 0;
     bool pf_split_ready = false;                 // pf_norm left the next GEMM's split input
     bool pf_glu_split = true;                    // XH_OPT_PREFILL_GLU_SPLIT: fused GLU -> split input
-    bool pf_attn_mfma = true;                    // XH_OPT_PREFILL_ATTN: 1 MFMA tiles, 0 per-token split kernel
+    int pf_attn_mode = 1;                        // XH_OPT_PREFILL_ATTN: 1 shared-tile MFMA (v1 for head_dim != 128),
+                                                 // 2 per-wave MFMA tiles, 0 per-token split kernel
     // T = pf_cap tokens (the pass length in use; pf_alloc)
     uint16_t* pf_xh = nullptr;                   // [2T][max K] f16 halves of a GEMM input (pf_alloc)
     uint16_t* pf_xl = nullptr;                   // [PF_TOK][max K] the split kernel's lo fragments
@@ -1042,12 +1043,22 @@ void pf_attn_t(xh_ctx* ctx, const AttnArgs& a, int n) {
 template <int HD, int QPK>
 void pf_fa_t(xh_ctx* ctx, const AttnArgs& a, int n, int pos0) {
     constexpr int TPW = 32 / QPK;
+    if constexpr (HD == 128) {
+        if (ctx->pf_attn_mode == 1) {
+            constexpr int NW = PF_FA_WAVES;
+            auto k = prefill_fa2_kernel<QPK, NW>;
+            ensure_lds((const void*)k);
+            hipLaunchKernelGGL(k, dim3(ctx->c.n_kv_heads, (n + NW * TPW - 1) / (NW * TPW)), dim3(64 * NW),
+                               fa_lds_bytes(), ctx->stream, a.q, a.kc, a.vc, a.out, n, pos0, ctx->q_dim, ctx->kv_dim);
+            return;
+        }
+    }
     hipLaunchKernelGGL((prefill_fa_kernel<HD, QPK>), dim3(ctx->c.n_kv_heads, (n + TPW - 1) / TPW), dim3(64), 0,
                        ctx->stream, a.q, a.kc, a.vc, a.out, n, pos0, ctx->q_dim, ctx->kv_dim);
 }
 bool pf_attn(xh_ctx* ctx, const AttnArgs& a, int n, int pos0) {
     const int hd = ctx->c.head_dim, qpk = ctx->qpk;
-    if (ctx->pf_attn_mfma) {
+    if (ctx->pf_attn_mode != 0) {
         if (hd == 128 && qpk == 4) pf_fa_t<128, 4>(ctx, a, n, pos0);
         else if (hd == 128 && qpk == 8) pf_fa_t<128, 8>(ctx, a, n, pos0);
         else if (hd == 64 && qpk == 4) pf_fa_t<64, 4>(ctx, a, n, pos0);
@@ -1896,7 +1907,7 @@ int xh_get_option(const xh_ctx* ctx, int option, int* value) {
         case XH_OPT_FUSE_ATTN_WO: *value = ctx->fuse_attn_wo ? 1 : 0; return 0;
         case XH_OPT_PREFILL: *value = ctx->prefill_batched ? ctx->prefill_gemm : 0; return 0;
         case XH_OPT_PREFILL_GLU_SPLIT: *value = ctx->pf_glu_split ? 1 : 0; return 0;
-        case XH_OPT_PREFILL_ATTN: *value = ctx->pf_attn_mfma ? 1 : 0; return 0;
+        case XH_OPT_PREFILL_ATTN: *value = ctx->pf_attn_mode; return 0;
         default: return XH_E_INVALID;
     }
 }
@@ -1919,8 +1930,8 @@ int xh_set_option(xh_ctx* ctx, int option, int value) {
             ctx->pf_glu_split = value != 0;
             return 0;
         case XH_OPT_PREFILL_ATTN:
-            if (value < 0 || value > 1) return set_err(ctx, XH_E_INVALID, "XH_OPT_PREFILL_ATTN: 0 or 1");
-            ctx->pf_attn_mfma = value != 0;
+            if (value < 0 || value > 2) return set_err(ctx, XH_E_INVALID, "XH_OPT_PREFILL_ATTN: 0, 1 or 2");
+            ctx->pf_attn_mode = value;
             return 0;
         default: return set_err(ctx, XH_E_INVALID, "unknown option %d", option);
     }
