@@ -197,8 +197,10 @@ int xh_set_graphs(xh_ctx* ctx, int enable);
  * f32 first, then split in the W2 GEMM's input pass (two launches).  Bit-identical results; a
  * debug knob so tests cover both routes. */
 /* XH_OPT_PREFILL_ATTN (default 1): the batched path's causal attention on MFMA tiles (32 query
- * rows x 32-slot K/V tiles per wave, running max/sum, q and p as exact f16 hi + lo pairs);
- * 0 = one workgroup per token and KV head, split-KV f32 FMA (the decode attention's blocks).
+ * rows x 32-slot K/V tiles per wave, running max/sum, q and p as exact f16 hi + lo pairs), the
+ * K/V tiles shared by the 4 waves of a workgroup through an LDS ring (head_dim 128); 2 = the same
+ * arithmetic with every wave reading its own tiles (bit-identical to 1); 0 = one workgroup per
+ * token and KV head, split-KV (the decode attention's blocks).
  * Option id 4 (XH_OPT_COL_KV_MAX, removed in round 3 with the column-form attention) is no
  * longer accepted: xh_set_option / xh_get_option return XH_E_INVALID for it. */
 enum xh_option { XH_OPT_FUSE_ATTN_WO = 1, XH_OPT_PREFILL = 2, XH_OPT_PREFILL_GLU_SPLIT = 3, XH_OPT_PREFILL_ATTN = 5 };

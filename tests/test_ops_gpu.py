@@ -101,6 +101,22 @@ def test_mha(head_dim, n_heads, n_kv, kv_len, msl):
     assert np.abs(got - cpu).max() < 2e-5, np.abs(got - cpu).max()
 
 
+@pytest.mark.parametrize("n_heads,n_kv", [(32, 8), (8, 8), (16, 8)])
+@pytest.mark.parametrize("kv_len", [257, 1000, 8191, 20001])
+def test_mha_long_splits(n_heads, n_kv, kv_len):
+    """Splits of 256..1024 slots at head_dim 128 with 4, 1 and 2 q heads per KV head (ragged
+    last rounds, many partials merged by the last split) against the oracle's per-head loop."""
+    rng = np.random.default_rng(kv_len + 7 * n_heads)
+    head_dim, msl = 128, 32768
+    kv_dim = n_kv * head_dim
+    kb = f16(rng.standard_normal((msl, kv_dim)).astype(np.float32))
+    vb = f16(rng.standard_normal((msl, kv_dim)).astype(np.float32))
+    q = (rng.standard_normal(n_heads * head_dim) * 0.5).astype(np.float32)
+    got = L.op_mha(kb, vb, q, head_dim, kv_len, msl, n_heads, n_kv)
+    cpu = O.mha(kb, vb, q, head_dim, kv_len, msl, n_heads, n_kv)
+    assert np.abs(got - cpu).max() < 2e-5, np.abs(got - cpu).max()
+
+
 def test_mha_peaked_softmax_and_32k():
     # one key dominates (forces the split max-rescale path), long context split over many blocks
     rng = np.random.default_rng(5)

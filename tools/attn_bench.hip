@@ -143,8 +143,8 @@ int main(int argc, char** argv) {
         run(k_stream<1024, 3, true>, 1024, ns, 0, "stream HM t1024 D3");
         run(k_round<1024>, 1024, ns, attn_smem_bytes(HD, QPK, T, ns, 1024), "round   t1024");
     }
-    for (int ns : {32, 64, 128}) {
-        if (quick && ns != 32) continue;
+    for (int ns : {16, 32, 64, 128}) {
+        if (quick && ns > 32) continue;
         const int T = attn_split_len(kv_len, ns, attn_min_t_partials(HD, 1024));
         run(k_round<1024>, 1024, ns, attn_smem_bytes(HD, QPK, T, ns, 1024), "round   t1024");
         run(k_signal<1024>, 1024, ns, attn_smem_bytes(HD, QPK, T, ns, 1024), "merged  t1024");

@@ -596,6 +596,45 @@ __global__ __launch_bounds__(ATTN_THREADS) void prefill_attn_kernel(AttnArgs a, 
     attn_block<HD, QPK, ATTN_THREADS, false>(a, blockIdx.x, blockIdx.y, smem, nullptr);
 }
 
+// One 32-slot tile of the prompt attention's online softmax (both kernels below): scores
+// s = st * (1 / row scale) * (1/sqrtf(hd)) (the first factor a power of two: one rounding), masked
+// past each row's pos on the diagonal tiles only (diag: wave-uniform), running max m over the
+// lane pair (l, l ^ 32), p = e^(s - m) split into exact f16 hi + lo (|p - hi - lo| <= 2^-25), O and
+// the running sum rescaled by e^(m_old - m) — skipped when it is 1 in every lane (exact: x * 1 = x).
+// e^x by v_exp_f32 of x log2(e) (__expf: <= 2e-6 relative at the x > -20 that carry weight).
+template <int NDT>
+__device__ __forceinline__ void fa_softmax_tile(const f32x16& st, const int b, const int pos, const int h,
+                                                const float sc, const bool diag, float& m, float& lsum,
+                                                f32x16 (&o)[NDT], f16x8 (&ph)[2], f16x8 (&pl)[2]) {
+    float sv[16];
+    float tm = -INFINITY;
+#pragma unroll
+    for (int r = 0; r < 16; r++) {
+        float v = st[r] * sc;
+        if (diag) v = b + (r & 3) + 8 * (r >> 2) + 4 * h <= pos ? v : -INFINITY;
+        sv[r] = v;
+        tm = fmaxf(tm, v);
+    }
+    tm = fmaxf(tm, __shfl_xor(tm, 32));
+    const float mn = fmaxf(m, tm);  // finite: slot 0 <= pos on the first tile
+    const float alpha = __expf(m - mn);
+    m = mn;
+    float ps = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; r++) {
+        const float p = __expf(sv[r] - mn);
+        ps += p;
+        const _Float16 hi = (_Float16)p;
+        ph[r >> 3][r & 7] = hi;
+        pl[r >> 3][r & 7] = (_Float16)(p - (float)hi);
+    }
+    lsum = lsum * alpha + ps;
+    if (!__all(alpha == 1.f)) {
+#pragma unroll
+        for (int dt = 0; dt < NDT; dt++) o[dt] *= alpha;
+    }
+}
+
 // ---- causal attention of a prompt pass on MFMA ------------------------------------------
 // Per token and head (src/infer.cpp:279-301 / :338): s_t = (q . K[t]) * (1/sqrtf(hd)) over slots
 // [0, pos], p = softmax(s) (max-subtract, expf), out = sum_t p_t V[t].  Computed flash-style
@@ -706,32 +745,8 @@ __global__ __launch_bounds__(64) void prefill_fa_kernel(const float* q, const ui
                 }
             }
         }
-        // online softmax over this lane's 16 slots and its partner's
-        float sv[16];
-        float tm = -INFINITY;
-#pragma unroll
-        for (int r = 0; r < 16; r++) {
-            const int slot = b + (r & 3) + 8 * (r >> 2) + 4 * h;
-            sv[r] = slot <= pos ? st[r] * inv_s * scale : -INFINITY;
-            tm = fmaxf(tm, sv[r]);
-        }
-        tm = fmaxf(tm, __shfl_xor(tm, 32));
-        const float mn = fmaxf(m, tm);  // finite: slot 0 <= pos on the first tile
-        const float alpha = expf(m - mn);
-        m = mn;
-        float ps = 0.f;
         f16x8 ph[2], pl[2];
-#pragma unroll
-        for (int r = 0; r < 16; r++) {
-            const float p = expf(sv[r] - mn);
-            ps += p;
-            const _Float16 hi = (_Float16)p;
-            ph[r >> 3][r & 7] = hi;
-            pl[r >> 3][r & 7] = (_Float16)(p - (float)hi);
-        }
-        lsum = lsum * alpha + ps;
-#pragma unroll
-        for (int dt = 0; dt < NDT; dt++) o[dt] *= alpha;
+        fa_softmax_tile<NDT>(st, b, pos, h, inv_s * scale, b + 31 > pos0 + t0, m, lsum, o, ph, pl);
         __syncthreads();  // V^T tile written
 #pragma unroll
         for (int s2 = 0; s2 < 2; s2++) {
@@ -889,32 +904,8 @@ __global__ __launch_bounds__(64 * NW, 2) void prefill_fa2_kernel(const float* q,
             st = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf, qh[ks], st, 0, 0, 0);
             st = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf, ql[ks], st, 0, 0, 0);
         }
-        // online softmax over this lane's 16 slots and its partner's (as prefill_fa_kernel)
-        float sv[16];
-        float tm = -INFINITY;
-#pragma unroll
-        for (int r = 0; r < 16; r++) {
-            const int slot = b + (r & 3) + 8 * (r >> 2) + 4 * h;
-            sv[r] = slot <= pos ? st[r] * inv_s * scale : -INFINITY;
-            tm = fmaxf(tm, sv[r]);
-        }
-        tm = fmaxf(tm, __shfl_xor(tm, 32));
-        const float mn = fmaxf(m, tm);  // finite: slot 0 <= pos on the first tile
-        const float alpha = expf(m - mn);
-        m = mn;
-        float ps = 0.f;
         f16x8 ph[2], pl[2];
-#pragma unroll
-        for (int r = 0; r < 16; r++) {
-            const float p = expf(sv[r] - mn);
-            ps += p;
-            const _Float16 hi = (_Float16)p;
-            ph[r >> 3][r & 7] = hi;
-            pl[r >> 3][r & 7] = (_Float16)(p - (float)hi);
-        }
-        lsum = lsum * alpha + ps;
-#pragma unroll
-        for (int dt = 0; dt < NDT; dt++) o[dt] *= alpha;
+        fa_softmax_tile<NDT>(st, b, pos, h, inv_s * scale, b + 31 > pos0 + t0, m, lsum, o, ph, pl);
         // O^T += V^T P^T: element e of the A fragment = slot 16 s2 + 8 (e >> 2) + 4 h + (e & 3)
 #pragma unroll
         for (int s2 = 0; s2 < 2; s2++) {

@@ -380,7 +380,10 @@ bool launch_attn(const AttnArgs& a, int hd, int qpk, int n_kv_heads, int t_max, 
 int attn_nsplit(int n_kv_heads, int max_seq_len) {
     // one split workgroup per CU at the longest context (tools/attn_bench.hip, 32k: 32 splits
     // per KV head 34.9 us vs 64 splits 39.0 us)
-    int ns = 256 / n_kv_heads;
+#ifndef ATTN_SPLIT_WGS
+#define ATTN_SPLIT_WGS 256
+#endif
+    int ns = ATTN_SPLIT_WGS / n_kv_heads;
     if (ns > 128) ns = 128;  // the merge holds <= 2 partials per lane
     const int cap = (max_seq_len + ATTN_MIN_T - 1) / ATTN_MIN_T;
     if (ns > cap) ns = cap;
@@ -722,6 +725,9 @@ int pf_alloc_split_attn(xh_ctx* ctx) {
 // reach it as their exact f16 image (pf_dequant): the torch-bundled hipBLASLt, loaded first
 // under the same soname in a process that imported torch, has no e4m3 / e5m2 kernels.  One
 // plan per (rows, K, n) holding the heuristic's candidates; *plan = nullptr when there are none.
+// At most PF_BLAS_MAX_PLANS plans per context (one per GEMM shape and pass length): a new pass length
+// past that runs on gemm16.h, so the map does not grow with every prompt length seen.
+constexpr size_t PF_BLAS_MAX_PLANS = 256;
 int blas_plan(xh_ctx* ctx, int rows, int K, int n, xh_ctx::BlasPlan** plan) {
     *plan = nullptr;
     if (!ctx->blas) {
@@ -733,6 +739,7 @@ int blas_plan(xh_ctx* ctx, int rows, int K, int n, xh_ctx::BlasPlan** plan) {
     }
     const std::vector<int> key{rows, K, n};
     auto it = ctx->blas_plans.find(key);
+    if (it == ctx->blas_plans.end() && ctx->blas_plans.size() >= PF_BLAS_MAX_PLANS) return 0;  // gemm16.h instead
     if (it == ctx->blas_plans.end()) {
         xh_ctx::BlasPlan& p = ctx->blas_plans[key];  // destroyed with the context, even half-built
         BLAS_TRY(ctx, hipblasLtMatmulDescCreate(&p.md, HIPBLAS_COMPUTE_32F, HIP_R_32F));
@@ -965,11 +972,17 @@ int pf_gemm(xh_ctx* ctx, const char* what, int dt, const void* w, int K, int row
         }
         ctx->pf_scaled = true;
         if (ctx->prefill_gemm == 4) {
-            // hi and lo rows as one B operand of 2n columns: partials [2][n][rows]
-            int rc = blas_gemm(ctx, w, K, rows, ctx->pf_xh, 2 * n, ctx->pf_part);
+            // hi and lo rows as one B operand of 2n columns: partials [2][n][rows]; a pass length
+            // hipBLASLt has no algorithm for runs on gemm16.h instead (same layout, same bound)
+            xh_ctx::BlasPlan* pp = nullptr;
+            int rc = blas_plan(ctx, rows, K, 2 * n, &pp);
             if (rc) return rc;
-            ks = 2;
-            return 0;
+            if (pp || K % MM_KMULT) {
+                rc = blas_gemm(ctx, w, K, rows, ctx->pf_xh, 2 * n, ctx->pf_part);
+                if (rc) return rc;
+                ks = 2;
+                return 0;
+            }
         }
         const int images = w_lo ? 2 : 1;
         const size_t cap = pf_part_floats(ctx, ctx->pf_cap);
