@@ -244,6 +244,8 @@ def cpu_baseline(w, c, prompt, gpu_logits0, gpu_tokens, n_decode, one_thread_tok
     ru0 = resource.getrusage(resource.RUSAGE_SELF)
     t0 = time.time()
     for i, tok in enumerate(hyd):
+        if i % 8 == 0:
+            progress(f"cpu baseline: hydrate token {i} / {len(hyd)}")
         om.forward(tok, pos0 + i, L.OUTPUT_LOGITS if i == len(hyd) - 1 else L.HYDRATE_KV_CACHE)
     t_hyd = time.time() - t0
     lg0 = om.logits()
@@ -252,7 +254,7 @@ def cpu_baseline(w, c, prompt, gpu_logits0, gpu_tokens, n_decode, one_thread_tok
     agree, disagree = 0, []
     t1 = time.time()
     for i in range(n_decode):
-        if i % 16 == 0:
+        if i % 16 == 0 or w["kv_prefill"]:
             progress(f"cpu baseline: decode token {i} / {n_decode} ({cores} threads)")
         lg = om.logits()
         ref_tok = O.sample_argmax(lg)
@@ -273,7 +275,8 @@ def cpu_baseline(w, c, prompt, gpu_logits0, gpu_tokens, n_decode, one_thread_tok
         nonlocal pos, nxt
         O.set_threads(threads)
         t = time.time()
-        for _ in range(n_tok):
+        for k in range(n_tok):
+            progress(f"cpu baseline: {threads}-thread sample, token {k} / {n_tok}")
             om.forward(gpu_tokens[nxt], pos, L.OUTPUT_LOGITS)
             pos += 1
             nxt += 1
@@ -288,6 +291,8 @@ def cpu_baseline(w, c, prompt, gpu_logits0, gpu_tokens, n_decode, one_thread_tok
     t2 = time.time()
     om64 = oracle(1)
     for i, tok in enumerate(hyd):
+        if i % 4 == 0:
+            progress(f"cpu baseline: fp64 evaluation, token {i} / {len(hyd)}")
         om64.forward(tok, pos0 + i, L.OUTPUT_LOGITS if i == len(hyd) - 1 else L.HYDRATE_KV_CACHE)
     lg64 = om64.logits()
     om64.close()

@@ -43,7 +43,7 @@ step bench 600 python3 bench.py
 step bench_f8 600 python3 bench.py --workload mistral-7b-f8
 fi
 if [ "$PART" != a ]; then
-step bench_32k 600 python3 bench.py --workload mistral-7b-f16-32k --steps 64
+step bench_32k 900 python3 bench.py --workload mistral-7b-f16-32k --steps 64 --cpu-tokens 8
 step bench_llama 600 python3 bench.py --workload llama3-8b-f16
 # SURVEY 8f-4 block formats (not BASELINE configs; the oracle's per-element block decode makes
 # a CPU sample slow, so none)
