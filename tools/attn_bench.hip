@@ -31,6 +31,19 @@ __global__ __launch_bounds__(THREADS) void k_round(const AttnArgs a, unsigned* d
     extern __shared__ __attribute__((aligned(16))) char smem[];
     attn_block<HD, QPK, THREADS, true>(a, blockIdx.x / a.nsplit, blockIdx.x % a.nsplit, smem, done);
 }
+// timeline of the long split (attn_block's stamps: 2 split known, 3 scores done, 6 softmax done,
+// 7 p.V done, 4 reduced, 5 partial drained), one record of 8 words per workgroup
+__device__ unsigned long long g_stamps[8 * 1024];
+template <int THREADS>
+__global__ __launch_bounds__(THREADS) void k_stamp(const AttnArgs a, unsigned* done) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    unsigned long long* d = g_stamps + 8 * blockIdx.x;
+    if (threadIdx.x == 0) d[0] = __builtin_amdgcn_s_memrealtime();
+    attn_block<HD, QPK, THREADS, false, attn_min_t_partials(HD, THREADS), NoWait, AddArrive, true>(
+        a, blockIdx.x / a.nsplit, blockIdx.x % a.nsplit, smem, done, d);
+    __syncthreads();
+    if (threadIdx.x == 0) d[1] = __builtin_amdgcn_s_memrealtime();
+}
 template <int THREADS>
 __global__ __launch_bounds__(THREADS) void k_signal(const AttnArgs a, unsigned* done) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -142,6 +155,27 @@ int main(int argc, char** argv) {
         run(k_stream<1024, 2, true>, 1024, ns, 0, "stream HM t1024 D2");
         run(k_stream<1024, 3, true>, 1024, ns, 0, "stream HM t1024 D3");
         run(k_round<1024>, 1024, ns, attn_smem_bytes(HD, QPK, T, ns, 1024), "round   t1024");
+    }
+    {
+        // timeline of one launch at 32 splits (100 MHz realtime counter: 10 ns ticks)
+        const int ns = 32;
+        const int T = attn_split_len(kv_len, ns, attn_min_t_partials(HD, 1024));
+        run(k_stamp<1024>, 1024, ns, attn_smem_bytes(HD, QPK, T, ns, 1024), "stamped t1024");
+        std::vector<unsigned long long> st(8 * NKV * ns);
+        CK(hipMemcpyFromSymbol(st.data(), HIP_SYMBOL(g_stamps), st.size() * 8));
+        unsigned long long t0 = ~0ull;
+        for (int b = 0; b < NKV * ns; b++) t0 = std::min(t0, st[8 * b]);
+        double acc[8] = {};
+        int cnt = 0;
+        for (int b = 0; b < NKV * ns; b++) {
+            const unsigned long long* d = &st[8 * b];
+            if (!d[3] || !d[6] || !d[7]) continue;
+            acc[0] += (d[0] - t0) * 0.01; acc[1] += (d[3] - d[0]) * 0.01; acc[2] += (d[6] - d[3]) * 0.01;
+            acc[3] += (d[7] - d[6]) * 0.01; acc[4] += (d[1] - d[7]) * 0.01; acc[5] += (d[1] - t0) * 0.01;
+            cnt++;
+        }
+        printf("  timeline (us, mean of %d splits): start %.2f, K pass %.2f, softmax %.2f, p.V pass %.2f, tail %.2f, end %.2f\n",
+               cnt, acc[0] / cnt, acc[1] / cnt, acc[2] / cnt, acc[3] / cnt, acc[4] / cnt, acc[5] / cnt);
     }
     for (int ns : {16, 32, 64, 128}) {
         if (quick && ns > 32) continue;

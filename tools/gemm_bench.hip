@@ -88,9 +88,11 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(dw, hw.data(), wmax * 2, hipMemcpyHostToDevice));
     struct Var { const char* name; void (*fn)(xalm::MmArgs); int lds; int bt; };
     const Var vars[] = {
-        {"b128g", xalm::mm_f16_kernel_t<64, 2, 4, 128>, xalm::MmCfg<64, 2, 128>::LDS, 128},
         {"m16g", xalm::mm_f16_kernel_t<64, 2, 12, 128>, xalm::MmCfg<64, 2, 128>::LDS, 128},
-        {"m16gpr", xalm::mm_f16_kernel_t<64, 2, 14, 128>, xalm::MmCfg<64, 2, 128>::LDS, 128},
+        {"t256b32", xalm::mm_f16_kernel_t<32, 3, 4, 256>, xalm::MmCfg<32, 3, 256>::LDS, 256},
+        {"t256m16", xalm::mm_f16_kernel_t<32, 3, 12, 256>, xalm::MmCfg<32, 3, 256>::LDS, 256},
+        {"t256m16s2", xalm::mm_f16_kernel_t<32, 2, 12, 256>, xalm::MmCfg<32, 2, 256>::LDS, 256},
+        {"m16b32s3", xalm::mm_f16_kernel_t<32, 3, 12, 128>, xalm::MmCfg<32, 3, 128>::LDS, 128},
     };
     const int NV = sizeof vars / sizeof vars[0];
     for (int v = 0; v < NV; v++)

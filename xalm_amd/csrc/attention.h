@@ -71,6 +71,15 @@ __device__ __forceinline__ void st_sc1(float* p, const float v) {
     __hip_atomic_store((uint32_t*)p, __builtin_bit_cast(uint32_t, v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations, not for its
+// global loads (__syncthreads() drains vmcnt too, which made every wave wait for the first V
+// round — a full HBM round trip — before the softmax: 2.5 us of a 32k split, tools/attn_bench)
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
 struct NoWait {
     __device__ void operator()() const {}
 };
@@ -103,7 +112,8 @@ __device__ __forceinline__ void attn_block(const AttnArgs& a, const int g, const
     constexpr int NO = QPK * HD;              // outputs of this block
     float* red = (float*)smem;                               // [WAVES][NO]
     float* ml = red + WAVES * NO;                            // [QPK][2] (+ flag)
-    float* sc = ml + ((2 * QPK + 4) & ~3);                   // [QPK][T]
+    float* xw = ml + ((2 * QPK + 4) & ~3);                   // [2][WAVES] softmax partials of each wave
+    float* sc = xw + 2 * WAVES;                              // [QPK][T]
     int* flag = (int*)(ml + 2 * QPK);
 
     const int kv_len = a.sp->kv_len;
@@ -195,25 +205,74 @@ __device__ __forceinline__ void attn_block(const AttnArgs& a, const int g, const
     // a split of one round re-reads its last row, unused)
     u32x4 vn[PREF];
     ld_round(vn, a.vc, t0 + STEP);
-    __syncthreads();
+    lds_barrier();  // the scores are in LDS; the V loads stay in flight across the softmax
     ATTN_STAMP(3);
 
     // ---- softmax statistics per head (max-subtract + expf, src/infer.cpp:280-297) ----
+    // WPH waves per head (all waves busy), each taking 256-score blocks: a lane holds 4
+    // consecutive scores per float4, so the LDS reads and the expf of a block are independent (a
+    // loop of one score per lane and iteration on one wave per head waited out an LDS round trip
+    // per score: 2.4 us of a 32k split, tools/attn_bench).  The per-wave max and sum combine in
+    // wave order through xw.  sc rows start 16-B aligned (T % 16 == 0); reads past len stay
+    // inside the row and are masked.
+    // (short splits of the fused launch keep one wave per head: no barrier between the passes)
+    constexpr int WPH = PARTIALS ? 1 : (WAVES / QPK > 0 ? WAVES / QPK : 1);
     const int len = t1 - t0;
-    for (int h = wid; h < QPK; h += WAVES) {
-        float m = -FLT_MAX;
-        for (int i = lane; i < len; i += 64) m = fmaxf(m, sc[h * T + i]);
+    const int sh = wid / WPH, sw = wid - sh * WPH;  // this wave's head and its share
+    float* row = sc + sh * T;
+    float m = -FLT_MAX;
+    if (sh < QPK) {
+        for (int i = 256 * sw + 4 * lane; i < len; i += 256 * WPH) {
+            const float4 v = *(const float4*)(row + i);
+            m = fmaxf(m, v.x);
+            if (i + 1 < len) m = fmaxf(m, v.y);
+            if (i + 2 < len) m = fmaxf(m, v.z);
+            if (i + 3 < len) m = fmaxf(m, v.w);
+        }
         m = wave_max(m);
+        if (WPH > 1 && lane == 0) xw[wid] = m;
+    }
+    if constexpr (WPH > 1) lds_barrier();
+    if (sh < QPK) {
+        if constexpr (WPH > 1) {
+            m = xw[sh * WPH];
+#pragma unroll
+            for (int k = 1; k < WPH; k++) m = fmaxf(m, xw[sh * WPH + k]);
+        }
         float l = 0.f;
-        for (int i = lane; i < len; i += 64) {
-            const float e = expf(sc[h * T + i] - m);
-            sc[h * T + i] = e;
-            l += e;
+        for (int i = 256 * sw + 4 * lane; i < len; i += 256 * WPH) {
+            const float4 v = *(const float4*)(row + i);
+            float4 e;
+            e.x = expf(v.x - m);
+            e.y = i + 1 < len ? expf(v.y - m) : 0.f;
+            e.z = i + 2 < len ? expf(v.z - m) : 0.f;
+            e.w = i + 3 < len ? expf(v.w - m) : 0.f;
+            *(float4*)(row + i) = e;
+            l += (e.x + e.y) + (e.z + e.w);
         }
         l = wave_sum(l);
-        if (lane == 0) { ml[2 * h] = m; ml[2 * h + 1] = l; }
+        if (lane == 0) {
+            if (WPH == 1) {
+                ml[2 * sh] = m;
+                ml[2 * sh + 1] = l;
+            } else {
+                xw[WAVES + wid] = l;
+            }
+        }
     }
-    __syncthreads();
+    lds_barrier();
+    if constexpr (WPH > 1) {
+        if (tid < QPK) {  // (m, l) per head, the waves' sums in wave order
+            float mm = xw[tid * WPH], l = xw[WAVES + tid * WPH];
+            for (int k = 1; k < WPH; k++) {
+                mm = fmaxf(mm, xw[tid * WPH + k]);
+                l += xw[WAVES + tid * WPH + k];
+            }
+            ml[2 * tid] = mm;
+            ml[2 * tid + 1] = l;
+        }
+    }
+    // (p . V reads only sc, complete at the barrier above; ml is read after the next barrier)
     ATTN_STAMP(6);
 
     // ---- p . V ----
@@ -439,7 +498,7 @@ __global__ __launch_bounds__(ATTN_THREADS) void attn_split_kernel(const AttnArgs
 inline size_t attn_smem_bytes(const int hd, const int qpk, const int t_max, const int nsplit,
                               const int threads = ATTN_THREADS) {
     const size_t scn = (size_t)qpk * (t_max > nsplit ? t_max : nsplit);
-    return sizeof(float) * ((size_t)(threads / 64) * qpk * hd + ((2 * qpk + 4) & ~3) + scn);
+    return sizeof(float) * ((size_t)(threads / 64) * qpk * hd + ((2 * qpk + 4) & ~3) + 2 * (threads / 64) + scn);
 }
 
 }  // namespace xalm

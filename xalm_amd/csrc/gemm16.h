@@ -197,7 +197,7 @@ __global__ __launch_bounds__(MM_THREADS, OCC) void mm_f16_kernel_t(const MmArgs 
         // cycles per FLOP, the chip holds a higher clock): 4 x 2RT tiles of 16 x 16 per wave; lane l
         // reads row l & 15 at chunk 4 q + (l >> 4) of a 32-deep step q (the same image stays
         // conflict-free: a lane group covers rows 0-3, 12-15 at one chunk and 4-11 at the next)
-        static_assert(BK == 64, "16x16x32 tiles read 64-deep image rows");
+        static_assert(BK % 32 == 0, "16x16x32 tiles read 32-deep steps");
         constexpr int RS = 2 * RT;  // 16-row tiles per wave
         const int l16 = lane & 15, q4 = lane >> 4;
         mm_f32x4 acc4[4][RS];
