@@ -366,7 +366,9 @@ def main():
 
     w = WORKLOADS[args.workload]
     c = make_config(w)
-    model = Model(c, device=local_rank)
+    # XALM_BENCH_DEVICE: every rank on one device (a multi-rank rehearsal on a one-GPU box)
+    device = int(os.environ.get("XALM_BENCH_DEVICE", local_rank))
+    model = Model(c, device=device)
     for kind, layer, dt, seed, mean, std in tensor_specs(w):
         model.upload_synthetic(kind, layer, dt, seed, mean, std)
 

@@ -89,10 +89,8 @@ int main(int argc, char** argv) {
     struct Var { const char* name; void (*fn)(xalm::MmArgs); int lds; int bt; };
     const Var vars[] = {
         {"m16g", xalm::mm_f16_kernel_t<64, 2, 12, 128>, xalm::MmCfg<64, 2, 128>::LDS, 128},
-        {"t256b32", xalm::mm_f16_kernel_t<32, 3, 4, 256>, xalm::MmCfg<32, 3, 256>::LDS, 256},
-        {"t256m16", xalm::mm_f16_kernel_t<32, 3, 12, 256>, xalm::MmCfg<32, 3, 256>::LDS, 256},
-        {"t256m16s2", xalm::mm_f16_kernel_t<32, 2, 12, 256>, xalm::MmCfg<32, 2, 256>::LDS, 256},
         {"m16b32s3", xalm::mm_f16_kernel_t<32, 3, 12, 128>, xalm::MmCfg<32, 3, 128>::LDS, 128},
+        {"m16b32o4", xalm::mm_f16_kernel_t<32, 2, 12, 128, 4>, xalm::MmCfg<32, 2, 128>::LDS, 128},
     };
     const int NV = sizeof vars / sizeof vars[0];
     for (int v = 0; v < NV; v++)
