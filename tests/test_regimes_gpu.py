@@ -351,10 +351,12 @@ def test_launch_structures_match_oracle(wdt, history, fuse):
 
 @pytest.mark.parametrize("attn", [1, 2, 0])
 @pytest.mark.parametrize("heads,kv_heads,head_dim,wdt", [(8, 2, 128, L.F16), (16, 2, 128, L.F16),
+                                                          (8, 8, 128, L.F16), (8, 4, 128, L.F16), (16, 2, 64, L.F16),
                                                           (8, 2, 64, L.F8_E4M3), (4, 2, 16, L.BF16)])
 def test_prompt_attention_in_two_prompts(heads, kv_heads, head_dim, wdt, attn):
     """xh_prefill's causal attention (XH_OPT_PREFILL_ATTN 1: MFMA tiles shared by a workgroup's
-    waves; 2: per-wave MFMA tiles; 0: per-token split kernel) at every instantiated head shape (QPK 4 / 8 / 2, head_dim 128 / 64 / 16), a prompt
+    waves; 2: per-wave MFMA tiles; 0: per-token split kernel) at the instantiated head shapes (QPK
+    1 / 2 / 4 / 8 — MHA through GQA —, head_dim 128 / 64 / 16), a prompt
     of 600 tokens followed by a second prompt of 300 at pos 600 (its rows attend over the first
     prompt's K/V), against the oracle's token loop: last logits and every K/V row.  f16
     weights run 512-token passes (attention over a pass boundary), bf16 64-token ones."""
@@ -378,7 +380,7 @@ def test_prompt_attention_in_two_prompts(heads, kv_heads, head_dim, wdt, attn):
             assert np.abs(a - b).max() <= 2e-3 * max(1.0, np.abs(b).max()), (layer, which)
 
 
-@pytest.mark.parametrize("heads,kv_heads", [(8, 2), (16, 2)])
+@pytest.mark.parametrize("heads,kv_heads", [(8, 2), (16, 2), (8, 8), (8, 4)])
 def test_prompt_attention_shared_tiles_bit_identical(heads, kv_heads):
     """XH_OPT_PREFILL_ATTN 1 (K/V tiles DMA'd once per workgroup, ring in LDS, V read by
     transposed LDS reads) runs prefill_fa_kernel's per-wave arithmetic unchanged: logits and

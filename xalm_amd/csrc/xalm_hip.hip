@@ -1069,24 +1069,42 @@ void pf_fa_t(xh_ctx* ctx, const AttnArgs& a, int n, int pos0) {
     hipLaunchKernelGGL((prefill_fa_kernel<HD, QPK>), dim3(ctx->c.n_kv_heads, (n + TPW - 1) / TPW), dim3(64), 0,
                        ctx->stream, a.q, a.kc, a.vc, a.out, n, pos0, ctx->q_dim, ctx->kv_dim);
 }
+// head shapes of the batched path's attention: head_dim 128 / 64 with 1, 2, 4 or 8 q heads per KV
+// head (MHA through GQA), and the test fixtures' head_dim 16 x 2
+bool pf_attn_shape(int hd, int qpk) {
+    return ((hd == 128 || hd == 64) && (qpk == 1 || qpk == 2 || qpk == 4 || qpk == 8)) || (hd == 16 && qpk == 2);
+}
+template <int HD>
+bool pf_attn_hd(xh_ctx* ctx, const AttnArgs& a, int n, int pos0, int qpk) {
+    if (ctx->pf_attn_mode != 0) {
+        switch (qpk) {
+            case 1: pf_fa_t<HD, 1>(ctx, a, n, pos0); return true;
+            case 2: pf_fa_t<HD, 2>(ctx, a, n, pos0); return true;
+            case 4: pf_fa_t<HD, 4>(ctx, a, n, pos0); return true;
+            case 8: pf_fa_t<HD, 8>(ctx, a, n, pos0); return true;
+            default: return false;
+        }
+    }
+    switch (qpk) {
+        case 1: pf_attn_t<HD, 1>(ctx, a, n); return true;
+        case 2: pf_attn_t<HD, 2>(ctx, a, n); return true;
+        case 4: pf_attn_t<HD, 4>(ctx, a, n); return true;
+        case 8: pf_attn_t<HD, 8>(ctx, a, n); return true;
+        default: return false;
+    }
+}
 bool pf_attn(xh_ctx* ctx, const AttnArgs& a, int n, int pos0) {
     const int hd = ctx->c.head_dim, qpk = ctx->qpk;
-    if (ctx->pf_attn_mode != 0) {
-        if (hd == 128 && qpk == 4) pf_fa_t<128, 4>(ctx, a, n, pos0);
-        else if (hd == 128 && qpk == 8) pf_fa_t<128, 8>(ctx, a, n, pos0);
-        else if (hd == 64 && qpk == 4) pf_fa_t<64, 4>(ctx, a, n, pos0);
-        else if (hd == 16 && qpk == 2) pf_fa_t<16, 2>(ctx, a, n, pos0);
-        else return false;
-        return true;
-    }
-    if (pf_alloc_split_attn(ctx)) return false;
+    if (!pf_attn_shape(hd, qpk)) return false;
     AttnArgs b = a;
-    b.part_o = ctx->pf_po; b.part_ml = ctx->pf_pml; b.counters = ctx->pf_cnt;
-    if (hd == 128 && qpk == 4) pf_attn_t<128, 4>(ctx, b, n);
-    else if (hd == 128 && qpk == 8) pf_attn_t<128, 8>(ctx, b, n);
-    else if (hd == 64 && qpk == 4) pf_attn_t<64, 4>(ctx, b, n);
-    else if (hd == 16 && qpk == 2) pf_attn_t<16, 2>(ctx, b, n);
-    else return false;
+    if (ctx->pf_attn_mode == 0) {
+        if (pf_alloc_split_attn(ctx)) return false;
+        b.part_o = ctx->pf_po; b.part_ml = ctx->pf_pml; b.counters = ctx->pf_cnt;
+    }
+    if (hd == 128) return pf_attn_hd<128>(ctx, b, n, pos0, qpk);
+    if (hd == 64) return pf_attn_hd<64>(ctx, b, n, pos0, qpk);
+    if (ctx->pf_attn_mode != 0) pf_fa_t<16, 2>(ctx, b, n, pos0);
+    else pf_attn_t<16, 2>(ctx, b, n);
     return true;
 }
 
@@ -1096,7 +1114,7 @@ bool pf_supported(const xh_ctx* ctx, int n, int pos0) {
     const xh_config& c = ctx->c;
     if (!ctx->prefill_batched || pos0 + n > c.max_seq_len) return false;
     const int hd = c.head_dim, qpk = ctx->qpk;
-    if (!((hd == 128 && (qpk == 4 || qpk == 8)) || (hd == 64 && qpk == 4) || (hd == 16 && qpk == 2))) return false;
+    if (!pf_attn_shape(hd, qpk)) return false;
     // every GEMM's K in whole chunk pairs of its decoder (f32-input kernel; the others need less)
     auto ok = [](int dt, int K) { return K % (2 * pf_elems(dt)) == 0; };
     for (const LayerW& w : ctx->L)
