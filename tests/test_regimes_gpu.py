@@ -403,3 +403,35 @@ def test_prompt_attention_shared_tiles_bit_identical(heads, kv_heads):
     assert np.array_equal(res[0][0], res[1][0])
     for a, b in zip(res[0][1], res[1][1]):
         assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("attn", [1, 2, 0])
+def test_prompt_over_long_history(attn):
+    """A 200-token prompt pass at pos0 = 12000 over a synthetic 12000-slot KV history (8 KV heads x
+    head_dim 128, 4 q per KV head): every token's attention walks ~375 K/V tiles through the
+    shared-tile ring (1), the per-wave tiles (2) or the split-KV kernel (0).  Last logits and the
+    pass's K/V rows against the oracle's token loop on the same weights and history."""
+    c = make_cfg(256, 512, 2, 32, 8, 128, 512, 16384)
+    gm, om = build_pair(c, L.F16)
+    gm.set_option(L.OPT_PREFILL_ATTN, attn)
+    history, n = 12000, 200
+    kv_dim = c.n_kv_heads * c.head_dim
+    for layer in range(c.n_layers):
+        for which in (0, 1):
+            seed = 3100 + 2 * layer + which
+            gm.kv_fill_synthetic(layer, which, 0, history, seed, 1.0)
+            om.set_kv(layer, which, 0, O.synthetic(history, kv_dim, L.F16, seed, 0.0, 1.0))
+    toks = [3 + (i * 29) % 500 for i in range(n)]
+    st = InferenceState(c)
+    gm.prefill(toks, history, st)
+    for i, tok in enumerate(toks):
+        om.forward(tok, history + i, L.OUTPUT_LOGITS if i == n - 1 else L.HYDRATE_KV_CACHE)
+    ref = om.logits()
+    assert np.abs(st.logits() - ref).max() <= bar(ref), float(np.abs(st.logits() - ref).max())
+    for layer in range(c.n_layers):
+        for which in (0, 1):
+            a = f16(gm.kv_read(layer, which, history, n))
+            b = f16(om.kv(layer, which)[history:history + n])
+            assert np.abs(a - b).max() <= 2e-3 * max(1.0, np.abs(b).max()), (layer, which)
+    gm.close()
+    om.close()
