@@ -779,8 +779,8 @@ __global__ __launch_bounds__(64) void prefill_fa_kernel(const float* q, const ui
 // prefill_fa_kernel's per-wave arithmetic, unchanged (same tiles, same MFMA order: the outputs
 // are bit-identical), but a workgroup of NW waves covers NW x 32 query rows of one KV head and
 // each 32-slot K / V tile goes L2 -> LDS ONCE for all of them, by global_load_lds_dwordx4, into a
-// ring of FA_NS stages issued FA_NS - 1 tiles ahead of the multiply (counted vmcnt + raw
-// s_barrier, as gemm16.h).  The single-wave kernel reads every K / V row once per wave from L2
+// ring of FA_NS stages of FA_TPS tiles, issued FA_NS - 1 stages ahead of the multiply (counted
+// vmcnt + raw s_barrier, as gemm16.h; two tiles per stage halve the barriers: +3.7 % at pos0 30719).  The single-wave kernel reads every K / V row once per wave from L2
 // with its loads exposed (one round trip per tile); here a tile costs one DMA per NW waves and
 // its latency hides under the previous tiles' MFMAs.
 // LDS image of a tile ([32 slots][128 f16], 256-B rows): 16-B chunk c of row r at byte
@@ -790,12 +790,18 @@ __global__ __launch_bounds__(64) void prefill_fa_kernel(const float* q, const ui
 // column (lane & 15) of the 4 rows), both conflict-free.  DMA writes are lane-linear, so the
 // chunk permutation is applied to the per-lane source address.  Slots past the workgroup's last
 // are clamped to it (valid rows; their p is 0 in every wave).
-constexpr int FA_NS = 3;                 // ring stages
+// a ring stage holds FA_TPS consecutive 32-slot K/V tiles (one counted wait + barrier per stage)
+#ifndef PF_FA_TPS
+#define PF_FA_TPS 2
+#endif
+constexpr int FA_TPS = PF_FA_TPS;
+constexpr int FA_NS = FA_TPS >= 2 ? 2 : 3;  // ring stages
 #ifndef PF_FA_WAVES
 #define PF_FA_WAVES 4                    // waves per workgroup
 #endif
 constexpr int FA_TILE_BYTES = 32 * 256;  // one K (or V) tile at head_dim 128
-__host__ __device__ constexpr int fa_lds_bytes() { return FA_NS * 2 * FA_TILE_BYTES; }
+constexpr int FA_STAGE_BYTES = FA_TPS * 2 * FA_TILE_BYTES;
+__host__ __device__ constexpr int fa_lds_bytes() { return FA_NS * FA_STAGE_BYTES; }
 __device__ __forceinline__ uint32_t fa_off(const int r, const int c) {
     return (uint32_t)(256 * r + 16 * (c ^ (((r & 3) << 2) | ((r >> 2) & 3))));
 }
@@ -808,8 +814,8 @@ __global__ __launch_bounds__(64 * NW, 2) void prefill_fa2_kernel(const float* q,
     constexpr int TPW = 32 / QPK;        // tokens per wave
     constexpr int KS = HD / 16;          // k steps of q . k
     constexpr int NDT = HD / 32;         // 32-row d tiles of O^T
-    constexpr int IPW = 16 / NW;         // DMA wave-instructions per wave per stage (16 x 1 KiB)
-    static_assert(32 % QPK == 0 && 16 % NW == 0, "prefill_fa2_kernel: shape");
+    constexpr int IPW = 16 * FA_TPS / NW;  // DMA wave-instructions per wave per stage (16 x 1 KiB per tile)
+    static_assert(32 % QPK == 0 && (16 * FA_TPS) % NW == 0, "prefill_fa2_kernel: shape");
     extern __shared__ __attribute__((aligned(16))) char fa_smem[];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int j32 = lane & 31, h = lane >> 5;
@@ -824,21 +830,24 @@ __global__ __launch_bounds__(64 * NW, 2) void prefill_fa2_kernel(const float* q,
     const int last_wg = pos0 + min(tb + NW * TPW, n) - 1;   // the workgroup's
     const float scale = 1.0f / sqrtf((float)HD);  // src/infer.cpp:338
 
-    // DMA sources: instruction i of this wave = image (i >> 3: K, V), rows 4 (i & 7) .. + 3
+    // DMA sources: instruction i of this wave = tile i >> 4 of the stage, image ((i >> 3) & 1: K, V),
+    // rows 4 (i & 7) .. + 3
     int drow[IPW], dch[IPW];
 #pragma unroll
     for (int k = 0; k < IPW; k++) {
         const int i = wv * IPW + k;
-        drow[k] = 4 * (i & 7) + (lane >> 4);
-        dch[k] = (lane & 15) ^ (((drow[k] & 3) << 2) | ((drow[k] >> 2) & 3));
+        drow[k] = 32 * (i >> 4) + 4 * (i & 7) + (lane >> 4);  // slot offset within the stage
+        const int r = drow[k] & 31;
+        dch[k] = (lane & 15) ^ (((r & 3) << 2) | ((r >> 2) & 3));
     }
     const int ntile = last_wg / 32 + 1;
-    auto issue = [&](const int stage, const int tile) {
-        char* base = fa_smem + stage * 2 * FA_TILE_BYTES;
+    const int nst = (ntile + FA_TPS - 1) / FA_TPS;
+    auto issue = [&](const int stage, const int st) {
+        char* base = fa_smem + stage * FA_STAGE_BYTES;
 #pragma unroll
         for (int k = 0; k < IPW; k++) {
             const int i = wv * IPW + k;
-            const uint16_t* src = (i < 8 ? kc : vc) + (size_t)min(32 * tile + drow[k], last_wg) * kv_dim +
+            const uint16_t* src = (((i >> 3) & 1) ? vc : kc) + (size_t)min(32 * FA_TPS * st + drow[k], last_wg) * kv_dim +
                                   (size_t)g * HD + 8 * dch[k];
             __builtin_amdgcn_global_load_lds((const void*)src,
                                              (__attribute__((address_space(3))) void*)(base + i * 1024), 16, 0, 0);
@@ -879,7 +888,7 @@ __global__ __launch_bounds__(64 * NW, 2) void prefill_fa2_kernel(const float* q,
     mm_wait_vm<0>();
 #pragma unroll
     for (int d = 0; d < FA_NS - 1; d++)
-        if (d < ntile) issue(d, d);
+        if (d < nst) issue(d, d);
 
     f32x16 o[NDT];
 #pragma unroll
@@ -887,14 +896,16 @@ __global__ __launch_bounds__(64 * NW, 2) void prefill_fa2_kernel(const float* q,
     float m = -INFINITY, lsum = 0.f;
     // tr-read addresses of this lane inside a V image (block rows r0 + q, d columns of dt)
     const int grp = lane >> 4, qq = (lane >> 2) & 3, pp = lane & 3;
-    for (int kt = 0; kt < ntile; kt++) {
-        mm_wait_ahead<IPW, FA_NS>(min(FA_NS - 2, ntile - 1 - kt));  // this wave's DMA of tile kt landed
-        __builtin_amdgcn_s_barrier();                                // ... every wave's; tile kt - 1 read
+    for (int ks = 0; ks < nst; ks++) {
+        mm_wait_ahead<IPW, FA_NS>(min(FA_NS - 2, nst - 1 - ks));  // this wave's DMA of stage ks landed
+        __builtin_amdgcn_s_barrier();                              // ... every wave's; stage ks - 1 read
         asm volatile("" ::: "memory");
-        if (kt + FA_NS - 1 < ntile) issue((kt + FA_NS - 1) % FA_NS, kt + FA_NS - 1);
-        const int b = 32 * kt;
-        if (b > last) continue;  // wave-uniform: past this wave's rows (it still issues its DMA share)
-        const char* kimg = fa_smem + (kt % FA_NS) * 2 * FA_TILE_BYTES;
+        if (ks + FA_NS - 1 < nst) issue((ks + FA_NS - 1) % FA_NS, ks + FA_NS - 1);
+#pragma unroll
+        for (int sub = 0; sub < FA_TPS; sub++) {
+        const int b = 32 * (ks * FA_TPS + sub);
+        if (b > last) break;  // wave-uniform: past this wave's rows (it still issues its DMA share)
+        const char* kimg = fa_smem + (ks % FA_NS) * FA_STAGE_BYTES + sub * 2 * FA_TILE_BYTES;
         const char* vimg = kimg + FA_TILE_BYTES;
         // S^T = K Q^T
         f32x16 st = f32x16{};
@@ -924,6 +935,7 @@ __global__ __launch_bounds__(64 * NW, 2) void prefill_fa2_kernel(const float* q,
                 o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vv, pl[s2], o[dt], 0, 0, 0);
             }
         }
+        }  // sub
     }
     const float l = lsum + __shfl_xor(lsum, 32);
     if (tq >= n) return;
