@@ -38,7 +38,7 @@ $(OBJ)/dt_launch_dt%.o: xalm_amd/csrc/dt_launch.hip $(HIP_HDR)
 	$(HIPCC) $(HIPFLAGS) -DPK_DT=$* -c -o $@ $<
 $(LIB)/libxalm_hip.so: $(OBJ)/xalm_hip.o $(PK_OBJS)
 	@mkdir -p $(LIB)
-	$(HIPCC) $(HIPFLAGS) -shared -o $@ $^ -lhipblaslt
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $^
 
 HOST_LIB_SRC := $(filter-out xalm_amd/host/main.cpp,$(HOST_SRC))
 $(LIB)/libxalm_host.so: $(HOST_LIB_SRC) $(HOST_HDR) $(LIB)/libxalm_hip.so

@@ -182,7 +182,7 @@ int xh_set_graphs(xh_ctx* ctx, int enable);
  * in one launch with an in-launch hand-off (attn_wo.h); 0 = two launches.  Same math. */
 /* XH_OPT_PREFILL (default 1): xh_prefill / xh_perplexity process the prompt in passes, each
  * weight matrix streamed once per pass into a GEMM.  1 = f16 and fp8 weights on the LDS-tiled MFMA
- * GEMM (gemm16.h) in passes of up to 1024 tokens (fp8 matrices through their exact f16 image),
+ * GEMM (gemm16.h) in passes of up to PF_TOK_MM = 2048 tokens (fp8 matrices through their exact f16 image),
  * activations as exact f16 hi + lo pairs under a power-of-two row scale (|x - (hi + lo) / s| <=
  * 2^-22 |x|, a 22-bit mantissa where the reference's f32 has 24), products exact, f32
  * accumulation in an order fixed by the tiling (the same bits on every run); other weight dtypes

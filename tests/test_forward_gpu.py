@@ -143,7 +143,7 @@ def test_prefill_matches_oracle(name, context, engine):
 @pytest.mark.parametrize("n", [1, 37, 64, 150])
 def test_batched_prefill_matches_oracle(name, n, mode):
     """xh_prefill's batched path (prefill.h / gemm16.h: the LDS-tiled f16 MFMA GEMM over passes of
-    <= 1024 tokens for f16 / fp8 weights, register-streaming MFMA GEMMs over passes of <= 64 tokens
+    <= PF_TOK_MM = 2048 tokens for f16 / fp8 weights, register-streaming MFMA GEMMs over passes of <= 64 tokens
     otherwise; causal attention on MFMA tiles) vs the oracle's token-by-token HYDRATE loop: last
     logits, every layer's K and V rows, and the greedy continuation after it.  mode 1: the default
     choice per dtype; 2: split-f16 register-streaming MFMA wherever the weights allow (f16 / fp8);

@@ -29,6 +29,28 @@ def test_library_exports_every_declared_symbol():
         assert hasattr(lib, n), n
 
 
+def test_library_needs_no_vendor_gemm():
+    """hipBLASLt (XH_OPT_PREFILL 4 only) is dlopen'ed on first use: it is not a link dependency
+    of the product library (ELF DT_NEEDED entries read straight from the file)."""
+    import struct
+    data = open(L.HIP_LIB_PATH, "rb").read()
+    assert data[:4] == b"\x7fELF" and data[4] == 2  # ELF64, little endian
+    shoff, = struct.unpack_from("<Q", data, 0x28)
+    shentsize, shnum = struct.unpack_from("<HH", data, 0x3A)
+    secs = [struct.unpack_from("<IIQQQQIIQQ", data, shoff + i * shentsize) for i in range(shnum)]
+    dyn = [s for s in secs if s[1] == 6]  # SHT_DYNAMIC
+    assert dyn
+    _, _, _, _, off, size, link, _, _, entsize = dyn[0]
+    stroff = secs[link][4]
+    needed = []
+    for i in range(size // entsize):
+        tag, val = struct.unpack_from("<qQ", data, off + i * entsize)
+        if tag == 1:  # DT_NEEDED
+            needed.append(data[stroff + val:data.index(b"\0", stroff + val)].decode())
+    assert any(n.startswith("libamdhip64") for n in needed), needed
+    assert not any("blas" in n for n in needed), needed
+
+
 def test_host_library_exports_declared_symbols():
     hdr = os.path.join(ROOT, "include", "xalm_host.h")
     so = os.path.join(ROOT, "xalm_amd", "lib", "libxalm_host.so")

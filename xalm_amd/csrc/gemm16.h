@@ -238,6 +238,7 @@ __global__ __launch_bounds__(MM_THREADS, OCC) void mm_f16_kernel_t(const MmArgs 
             if (d < nk) issue(d, d);
         for (int kt = 0; kt < nk; kt++) {
             mm_wait_ahead<C::LPS, NS>(min(NS - 2, nk - 1 - kt));
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // own ds_reads of the refilled stage retired
             __builtin_amdgcn_s_barrier();
             asm volatile("" ::: "memory");
             if (kt + NS - 1 < nk) issue((kt + NS - 1) % NS, kt + NS - 1);
@@ -317,6 +318,7 @@ __global__ __launch_bounds__(MM_THREADS, OCC) void mm_f16_kernel_t(const MmArgs 
         if (d < nk) issue(d, d);
     for (int kt = 0; kt < nk; kt++) {
         mm_wait_ahead<C::LPS, NS>(min(NS - 2, nk - 1 - kt));  // this wave's DMA of step kt landed
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // own ds_reads of the refilled stage retired
         __builtin_amdgcn_s_barrier();                          // ... every wave's; stage kt - 1 read
         asm volatile("" ::: "memory");
         if (kt + NS - 1 < nk) issue((kt + NS - 1) % NS, kt + NS - 1);

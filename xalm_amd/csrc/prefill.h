@@ -898,6 +898,7 @@ __global__ __launch_bounds__(64 * NW, 2) void prefill_fa2_kernel(const float* q,
     const int grp = lane >> 4, qq = (lane >> 2) & 3, pp = lane & 3;
     for (int ks = 0; ks < nst; ks++) {
         mm_wait_ahead<IPW, FA_NS>(min(FA_NS - 2, nst - 1 - ks));  // this wave's DMA of stage ks landed
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // own ds_reads of the refilled stage retired
         __builtin_amdgcn_s_barrier();                              // ... every wave's; stage ks - 1 read
         asm volatile("" ::: "memory");
         if (ks + FA_NS - 1 < nst) issue((ks + FA_NS - 1) % FA_NS, ks + FA_NS - 1);

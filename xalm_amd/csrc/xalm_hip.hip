@@ -23,7 +23,8 @@
 // LDS-DMA stream, qkv+attention+Wo, column-form attention — measured slower and were removed;
 // DESIGN.md §4.5 / §4.9 keep the measurements.)
 #include <hip/hip_runtime.h>
-#include <hipblaslt/hipblaslt.h>
+#include <dlfcn.h>
+#include <hipblaslt/hipblaslt.h>  // types only: the library is dlopen'ed (blas_api)
 #include <fcntl.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
@@ -712,6 +713,48 @@ int pf_alloc_split_attn(xh_ctx* ctx) {
     return 0;
 }
 
+// hipBLASLt serves only XH_OPT_PREFILL 4 (the vendor GEMM in place of gemm16.h).  Its entry
+// points are resolved on first use with dlopen / dlsym, so libxalm_hip.so has no link
+// dependency on it (a process that already loaded a copy, e.g. torch's, gets that copy by
+// soname); without it, mode 4 fails with an error and everything else is unaffected.
+struct BlasApi {
+#define XH_BLAS_FN(name) decltype(&hipblasLt##name) name = nullptr;
+    XH_BLAS_FN(Create) XH_BLAS_FN(Destroy) XH_BLAS_FN(MatmulDescCreate) XH_BLAS_FN(MatmulDescDestroy)
+    XH_BLAS_FN(MatmulDescSetAttribute) XH_BLAS_FN(MatrixLayoutCreate) XH_BLAS_FN(MatrixLayoutDestroy)
+    XH_BLAS_FN(MatmulPreferenceCreate) XH_BLAS_FN(MatmulPreferenceDestroy) XH_BLAS_FN(MatmulPreferenceSetAttribute)
+    XH_BLAS_FN(MatmulAlgoGetHeuristic) XH_BLAS_FN(Matmul)
+#undef XH_BLAS_FN
+    bool ok = false;
+    std::string err;
+};
+const BlasApi* blas_api(std::string* why = nullptr) {
+    static BlasApi api;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        void* h = nullptr;
+        for (const char* so : {"libhipblaslt.so.1", "libhipblaslt.so", "/opt/rocm/lib/libhipblaslt.so.1"})
+            if ((h = dlopen(so, RTLD_NOW | RTLD_LOCAL))) break;
+        if (!h) {
+            const char* e = dlerror();
+            api.err = e ? e : "dlopen failed";
+            return;
+        }
+        bool all = true;
+#define XH_BLAS_SYM(name)                                                                \
+        api.name = reinterpret_cast<decltype(api.name)>(dlsym(h, "hipblasLt" #name)); \
+        all = all && api.name;
+        XH_BLAS_SYM(Create) XH_BLAS_SYM(Destroy) XH_BLAS_SYM(MatmulDescCreate) XH_BLAS_SYM(MatmulDescDestroy)
+        XH_BLAS_SYM(MatmulDescSetAttribute) XH_BLAS_SYM(MatrixLayoutCreate) XH_BLAS_SYM(MatrixLayoutDestroy)
+        XH_BLAS_SYM(MatmulPreferenceCreate) XH_BLAS_SYM(MatmulPreferenceDestroy) XH_BLAS_SYM(MatmulPreferenceSetAttribute)
+        XH_BLAS_SYM(MatmulAlgoGetHeuristic) XH_BLAS_SYM(Matmul)
+#undef XH_BLAS_SYM
+        api.ok = all;
+        if (!all) api.err = "hipBLASLt: missing entry points";
+    });
+    if (why) *why = api.err;
+    return api.ok ? &api : nullptr;
+}
+
 #define BLAS_TRY(ctx, expr)                                                                          \
     do {                                                                                             \
         hipblasStatus_t _s = (expr);                                                                 \
@@ -730,8 +773,10 @@ int pf_alloc_split_attn(xh_ctx* ctx) {
 constexpr size_t PF_BLAS_MAX_PLANS = 256;
 int blas_plan(xh_ctx* ctx, int rows, int K, int n, xh_ctx::BlasPlan** plan) {
     *plan = nullptr;
+    std::string why;
+    if (!blas_api(&why)) return set_err(ctx, XH_E_HIP, "XH_OPT_PREFILL 4 needs hipBLASLt: %s", why.c_str());
     if (!ctx->blas) {
-        BLAS_TRY(ctx, hipblasLtCreate(&ctx->blas));
+        BLAS_TRY(ctx, blas_api()->Create(&ctx->blas));
         char* ws = nullptr;
         int rc = dmalloc(ctx, &ws, PF_BLAS_WS);
         if (rc) return rc;
@@ -742,24 +787,24 @@ int blas_plan(xh_ctx* ctx, int rows, int K, int n, xh_ctx::BlasPlan** plan) {
     if (it == ctx->blas_plans.end() && ctx->blas_plans.size() >= PF_BLAS_MAX_PLANS) return 0;  // gemm16.h instead
     if (it == ctx->blas_plans.end()) {
         xh_ctx::BlasPlan& p = ctx->blas_plans[key];  // destroyed with the context, even half-built
-        BLAS_TRY(ctx, hipblasLtMatmulDescCreate(&p.md, HIPBLAS_COMPUTE_32F, HIP_R_32F));
+        BLAS_TRY(ctx, blas_api()->MatmulDescCreate(&p.md, HIPBLAS_COMPUTE_32F, HIP_R_32F));
         const hipblasOperation_t opT = HIPBLAS_OP_T, opN = HIPBLAS_OP_N;
-        BLAS_TRY(ctx, hipblasLtMatmulDescSetAttribute(p.md, HIPBLASLT_MATMUL_DESC_TRANSA, &opT, sizeof opT));
-        BLAS_TRY(ctx, hipblasLtMatmulDescSetAttribute(p.md, HIPBLASLT_MATMUL_DESC_TRANSB, &opN, sizeof opN));
-        BLAS_TRY(ctx, hipblasLtMatrixLayoutCreate(&p.la, HIP_R_16F, K, rows, K));
-        BLAS_TRY(ctx, hipblasLtMatrixLayoutCreate(&p.lb, HIP_R_16F, K, n, K));
-        BLAS_TRY(ctx, hipblasLtMatrixLayoutCreate(&p.lc, HIP_R_32F, rows, n, rows));
+        BLAS_TRY(ctx, blas_api()->MatmulDescSetAttribute(p.md, HIPBLASLT_MATMUL_DESC_TRANSA, &opT, sizeof opT));
+        BLAS_TRY(ctx, blas_api()->MatmulDescSetAttribute(p.md, HIPBLASLT_MATMUL_DESC_TRANSB, &opN, sizeof opN));
+        BLAS_TRY(ctx, blas_api()->MatrixLayoutCreate(&p.la, HIP_R_16F, K, rows, K));
+        BLAS_TRY(ctx, blas_api()->MatrixLayoutCreate(&p.lb, HIP_R_16F, K, n, K));
+        BLAS_TRY(ctx, blas_api()->MatrixLayoutCreate(&p.lc, HIP_R_32F, rows, n, rows));
         hipblasLtMatmulPreference_t pref;
-        BLAS_TRY(ctx, hipblasLtMatmulPreferenceCreate(&pref));
+        BLAS_TRY(ctx, blas_api()->MatmulPreferenceCreate(&pref));
         size_t wss = PF_BLAS_WS;
         constexpr int NH = 8;
         hipblasLtMatmulHeuristicResult_t heur[NH];
         int nret = 0;
-        hipblasStatus_t st = hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES,
+        hipblasStatus_t st = blas_api()->MatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES,
                                                                    &wss, sizeof wss);
         if (st == HIPBLAS_STATUS_SUCCESS)
-            st = hipblasLtMatmulAlgoGetHeuristic(ctx->blas, p.md, p.la, p.lb, p.lc, p.lc, pref, NH, heur, &nret);
-        hipblasLtMatmulPreferenceDestroy(pref);
+            st = blas_api()->MatmulAlgoGetHeuristic(ctx->blas, p.md, p.la, p.lb, p.lc, p.lc, pref, NH, heur, &nret);
+        blas_api()->MatmulPreferenceDestroy(pref);
         for (int i = 0; st == HIPBLAS_STATUS_SUCCESS && i < nret; i++) p.cands.push_back(heur[i].algo);
         p.ready = true;
         it = ctx->blas_plans.find(key);
@@ -778,7 +823,7 @@ int blas_gemm(xh_ctx* ctx, const void* w, int K, int rows, const uint16_t* x, in
     if (rc) return rc;
     if (!pp) return set_err(ctx, XH_E_HIP, "hipBLASLt: no algorithm for %d x %d x %d", rows, K, n);
     const float alpha = 1.f, beta = 0.f;
-    BLAS_TRY(ctx, hipblasLtMatmul(ctx->blas, pp->md, &alpha, w, pp->la, x, pp->lb, &beta, y, pp->lc, y, pp->lc,
+    BLAS_TRY(ctx, blas_api()->Matmul(ctx->blas, pp->md, &alpha, w, pp->la, x, pp->lb, &beta, y, pp->lc, y, pp->lc,
                                   &pp->cands[0], ctx->blas_ws, PF_BLAS_WS, ctx->stream));
     return 0;
 }
@@ -1093,19 +1138,22 @@ bool pf_attn_hd(xh_ctx* ctx, const AttnArgs& a, int n, int pos0, int qpk) {
         default: return false;
     }
 }
-bool pf_attn(xh_ctx* ctx, const AttnArgs& a, int n, int pos0) {
+// 0, XH_E_INVALID for a head shape with no prompt attention, or the split buffers' allocation error
+int pf_attn(xh_ctx* ctx, const AttnArgs& a, int n, int pos0) {
     const int hd = ctx->c.head_dim, qpk = ctx->qpk;
-    if (!pf_attn_shape(hd, qpk)) return false;
+    if (!pf_attn_shape(hd, qpk)) return set_err(ctx, XH_E_INVALID, "prefill: head shape not instantiated");
     AttnArgs b = a;
     if (ctx->pf_attn_mode == 0) {
-        if (pf_alloc_split_attn(ctx)) return false;
+        const int rc = pf_alloc_split_attn(ctx);  // keeps dmalloc's code and message
+        if (rc) return rc;
         b.part_o = ctx->pf_po; b.part_ml = ctx->pf_pml; b.counters = ctx->pf_cnt;
     }
-    if (hd == 128) return pf_attn_hd<128>(ctx, b, n, pos0, qpk);
-    if (hd == 64) return pf_attn_hd<64>(ctx, b, n, pos0, qpk);
-    if (ctx->pf_attn_mode != 0) pf_fa_t<16, 2>(ctx, b, n, pos0);
+    bool ok = true;
+    if (hd == 128) ok = pf_attn_hd<128>(ctx, b, n, pos0, qpk);
+    else if (hd == 64) ok = pf_attn_hd<64>(ctx, b, n, pos0, qpk);
+    else if (ctx->pf_attn_mode != 0) pf_fa_t<16, 2>(ctx, b, n, pos0);
     else pf_attn_t<16, 2>(ctx, b, n);
-    return true;
+    return ok ? 0 : set_err(ctx, XH_E_INVALID, "prefill: head shape not instantiated");
 }
 
 // Whether the batched path covers this prompt (else the per-token loop): no ring wrap inside
@@ -1173,7 +1221,7 @@ int prefill_batched(xh_ctx* ctx, const int* tokens, int n, int pos0, int want_lo
             aa.q = ctx->pf_q; aa.out = ctx->pf_att;
             // splits for this pass's longest row (attn_block: >= ATTN_MIN_T slots per split)
             aa.nsplit = std::min(ctx->nsplit, std::max(1, (p0 + m + ATTN_MIN_T - 1) / ATTN_MIN_T));
-            if (!pf_attn(ctx, aa, m, p0)) return set_err(ctx, XH_E_INVALID, "prefill: head shape not instantiated");
+            if ((rc = pf_attn(ctx, aa, m, p0))) return rc;
             if ((rc = pf_gemm(ctx, "wo", kdt(w.wo_dt, w.wo_x), w.wo, ctx->q_dim, c.dim, ctx->pf_att, m, ks))) return rc;
             e = PfEpiArgs{};
             e.ks = ks; e.n = m; e.rows = c.dim; e.epi = EPI_RESID; e.out = ctx->pf_x;
@@ -1399,10 +1447,10 @@ void xh_destroy(xh_ctx* ctx) {
     for (auto& kv : ctx->blas_plans) {
         const xh_ctx::BlasPlan& p = kv.second;
         for (hipblasLtMatrixLayout_t l : {p.la, p.lb, p.lc})
-            if (l) hipblasLtMatrixLayoutDestroy(l);
-        if (p.md) hipblasLtMatmulDescDestroy(p.md);
+            if (l) blas_api()->MatrixLayoutDestroy(l);
+        if (p.md) blas_api()->MatmulDescDestroy(p.md);
     }
-    if (ctx->blas) hipblasLtDestroy(ctx->blas);
+    if (ctx->blas) blas_api()->Destroy(ctx->blas);
     hipFree(ctx->blas_ws);
     hipFree(ctx->sink_cos); hipFree(ctx->sink_sin); hipFree(ctx->sp); hipFree(ctx->dec_tokens);
     if (ctx->sp_host) hipHostFree(ctx->sp_host);
