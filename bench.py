@@ -71,13 +71,15 @@ def make_config(w):
     return c
 
 
-def tensor_specs(w):
+def tensor_specs(w, seed_shift=0):
     """(kind, layer, dtype, seed, mean, std) of every tensor; SURVEY §8d synthetic recipe:
-    matrices N(0,0.02^2), norms 1+N(0,0.01^2) bf16, embedding rows N(0,1)."""
-    specs = [(L.EMBED, 0, w["edt"], 1001, 0.0, 1.0), (L.FINAL_NORM, 0, L.BF16, 1002, 1.0, 0.01),
-             (L.WCLS, 0, w["cdt"], 1003, 0.0, 0.02)]
+    matrices N(0,0.02^2), norms 1+N(0,0.01^2) bf16, embedding rows N(0,1).  seed_shift: another
+    draw of the same recipe (a second weight seed for the parity tests)."""
+    z = seed_shift
+    specs = [(L.EMBED, 0, w["edt"], 1001 + z, 0.0, 1.0), (L.FINAL_NORM, 0, L.BF16, 1002 + z, 1.0, 0.01),
+             (L.WCLS, 0, w["cdt"], 1003 + z, 0.0, 0.02)]
     for layer in range(w["layers"]):
-        base = 10_000 + 100 * layer
+        base = 10_000 + 100 * layer + z
         specs += [(L.ATTN_NORM, layer, L.BF16, base + 1, 1.0, 0.01), (L.FFN_NORM, layer, L.BF16, base + 2, 1.0, 0.01)]
         for k in (L.WQ, L.WK, L.WV, L.WO, L.W1, L.W2, L.W3):
             specs.append((k, layer, w["wdt"], base + 10 + k, 0.0, 0.02))
@@ -251,6 +253,8 @@ def cpu_baseline(w, c, prompt, gpu_logits0, gpu_tokens, n_decode, one_thread_tok
     lg0 = om.logits()
     # teacher-forced on the GPU's tokens so both sides see identical inputs
     pos = pos0 + len(hyd)
+    # bytes the decode tokens move (Model::active_bytes, src/model.cpp:12-35): the CPU's GB/s
+    dec_bytes = sum(om.active_bytes(pos + i) for i in range(n_decode))
     agree, disagree = 0, []
     t1 = time.time()
     for i in range(n_decode):
@@ -300,6 +304,8 @@ def cpu_baseline(w, c, prompt, gpu_logits0, gpu_tokens, n_decode, one_thread_tok
     O.set_threads(share)
     cpu = host_cpu_info()
     return dict(value=round(n_decode / t_dec, 3), unit="tok/s", cores=cores, kind="port",
+                achieved_GBps=round(dec_bytes / t_dec / 1e9, 1),
+                isa={2: "AVX-512 (run-time dispatch)", 1: "AVX2/FMA/F16C", 0: "scalar"}[O.isa()],
                 cpu_model=cpu["model"], host_physical_cores=cpu["physical_cores"],
                 host_logical_cpus=cpu["logical_cpus"], affinity_cpus=cpu["affinity_cpus"], cgroup_cpu_quota=quota,
                 threads_note="OpenMP threads = the physical cores in this process's affinity mask (capped by a "

@@ -41,7 +41,7 @@ def _load():
             "xo_f16_to_f32": (ctypes.c_float, [ctypes.c_uint16]),
             "xo_sample_argmax": (_I, [_P, _I]), "xo_sample_prob": (ctypes.c_float, [_P, _I, _I]),
             "xo_num_threads": (_I, []), "xo_set_threads": (None, [_I]),
-            "xo_set_matmul_order": (None, [_I]), "xo_matmul_order": (_I, []),
+            "xo_set_matmul_order": (None, [_I]), "xo_matmul_order": (_I, []), "xo_isa": (_I, []),
             "xo_fill_synthetic": (None, [_P, _SZ, _SZ, _I, ctypes.c_uint64, ctypes.c_float, ctypes.c_float]),
             "xo_set_precision": (None, [_P, _I]), "xo_precision": (_I, [_P]),
         }
@@ -211,10 +211,15 @@ def set_threads(n):
 
 
 def set_matmul_order(order):
-    """f16 matmul in-row order: 0 = 8-wide FMA lanes (default), 1 = sequential.  Both read the
+    """f16 / fp8 matmul in-row order: 0 = 8-wide FMA lanes (default), 1 = sequential.  Both read the
     reference's `omp simd` row loop (src/infer.cpp:104-135) validly; their difference is the
     reference algorithm's own rounding-order sensitivity."""
     _load().xo_set_matmul_order(int(order))
+
+
+def isa():
+    """the instruction set of the lanes-order matvec: 2 = AVX-512 (run-time dispatch), 1 = AVX2"""
+    return int(_load().xo_isa())
 
 
 def matmul_order():

@@ -6,7 +6,7 @@
  * This file is the checker for the HIP path and the timed `-d cpu` baseline; nothing in
  * the product links it (see xalm_oracle.h).
  *
- * Build: oracle/Makefile  (gcc -O3 -fopenmp -mavx2 -mfma -mf16c)
+ * Build: oracle/Makefile  (gcc -O3 -fopenmp -mavx2 -mfma -mf16c; AVX-512 forms picked at run time)
  */
 #include "xalm_oracle.h"
 
@@ -173,36 +173,124 @@ int xo_matmul_order(void) {
     if (scalar_order < 0) scalar_order = getenv("XO_MATMUL_SCALAR") && atoi(getenv("XO_MATMUL_SCALAR"));
     return scalar_order;
 }
+#ifdef XO_SIMD
+/* Row dot products in the "lanes" order: four 8-wide FMA accumulators over the column blocks
+ * j, j+8, j+16, j+24 of every 32, summed (a0 + a1) + (a2 + a3), then horizontally, then the
+ * tail sequentially.  The AVX-512 forms hold [a0 | a1] and [a2 | a3] in two 16-wide registers:
+ * every lane sees the same FMAs in the same order, so both forms give the same bits; the host's
+ * ISA is picked at run time (BASELINE.md §3 asks for -march=native; the library must also run
+ * on hosts without AVX-512).  fp8 codes decode by the reference's bit formula (f8_t::to_float,
+ * src/types.h:302-314), 8 or 16 at a time. */
+static inline float hsum8(const __m256 a0, const __m256 a1, const __m256 a2, const __m256 a3) {
+    const __m256 s = _mm256_add_ps(_mm256_add_ps(a0, a1), _mm256_add_ps(a2, a3));
+    __m128 s4 = _mm_add_ps(_mm256_castps256_ps128(s), _mm256_extractf128_ps(s, 1));
+    s4 = _mm_hadd_ps(s4, s4);
+    s4 = _mm_hadd_ps(s4, s4);
+    return _mm_cvtss_f32(s4);
+}
+static inline __m256 f8x8(const uint8_t* p, const int e5m2) {
+    const __m256i b = _mm256_cvtepu8_epi32(_mm_loadl_epi64((const __m128i*)p));
+    const __m256i sg = _mm256_slli_epi32(_mm256_and_si256(b, _mm256_set1_epi32(0x80)), 24);
+    const __m256i mg = _mm256_and_si256(b, _mm256_set1_epi32(0x7f));
+    const __m256i u = _mm256_or_si256(sg, e5m2 ? _mm256_slli_epi32(mg, 21) : _mm256_slli_epi32(mg, 20));
+    return _mm256_mul_ps(_mm256_castsi256_ps(u), _mm256_set1_ps(e5m2 ? 0x1p112f : 0x1p120f));
+}
+static float dot_lanes_avx2(const void* rowp, const float* x, const int n, const int dtype) {
+    __m256 a0 = _mm256_setzero_ps(), a1 = _mm256_setzero_ps(), a2 = _mm256_setzero_ps(), a3 = _mm256_setzero_ps();
+    int j = 0;
+    if (dtype == XH_F16) {
+        const uint16_t* row = (const uint16_t*)rowp;
+        for (; j + 32 <= n; j += 32) {
+            a0 = _mm256_fmadd_ps(_mm256_cvtph_ps(_mm_loadu_si128((const __m128i*)(row + j))), _mm256_loadu_ps(x + j), a0);
+            a1 = _mm256_fmadd_ps(_mm256_cvtph_ps(_mm_loadu_si128((const __m128i*)(row + j + 8))), _mm256_loadu_ps(x + j + 8), a1);
+            a2 = _mm256_fmadd_ps(_mm256_cvtph_ps(_mm_loadu_si128((const __m128i*)(row + j + 16))), _mm256_loadu_ps(x + j + 16), a2);
+            a3 = _mm256_fmadd_ps(_mm256_cvtph_ps(_mm_loadu_si128((const __m128i*)(row + j + 24))), _mm256_loadu_ps(x + j + 24), a3);
+        }
+        float val = hsum8(a0, a1, a2, a3);
+        for (; j < n; j++) val += xo_f16_to_f32(row[j]) * x[j];
+        return val;
+    }
+    const uint8_t* row = (const uint8_t*)rowp;
+    const int e5 = dtype == XH_F8_E5M2;
+    for (; j + 32 <= n; j += 32) {
+        a0 = _mm256_fmadd_ps(f8x8(row + j, e5), _mm256_loadu_ps(x + j), a0);
+        a1 = _mm256_fmadd_ps(f8x8(row + j + 8, e5), _mm256_loadu_ps(x + j + 8), a1);
+        a2 = _mm256_fmadd_ps(f8x8(row + j + 16, e5), _mm256_loadu_ps(x + j + 16), a2);
+        a3 = _mm256_fmadd_ps(f8x8(row + j + 24, e5), _mm256_loadu_ps(x + j + 24), a3);
+    }
+    float val = hsum8(a0, a1, a2, a3);
+    for (; j < n; j++) val += (e5 ? f8e5m2_to_f32(row[j]) : f8e4m3_to_f32(row[j])) * x[j];
+    return val;
+}
+#define XO_AVX512 __attribute__((target("avx512f,avx512bw,avx512vl,avx2,fma,f16c")))
+XO_AVX512 static inline __m512 f8x16(const uint8_t* p, const int e5m2) {
+    const __m512i b = _mm512_cvtepu8_epi32(_mm_loadu_si128((const __m128i*)p));
+    const __m512i sg = _mm512_slli_epi32(_mm512_and_si512(b, _mm512_set1_epi32(0x80)), 24);
+    const __m512i mg = _mm512_and_si512(b, _mm512_set1_epi32(0x7f));
+    const __m512i u = _mm512_or_si512(sg, e5m2 ? _mm512_slli_epi32(mg, 21) : _mm512_slli_epi32(mg, 20));
+    return _mm512_mul_ps(_mm512_castsi512_ps(u), _mm512_set1_ps(e5m2 ? 0x1p112f : 0x1p120f));
+}
+XO_AVX512 static float dot_lanes_avx512(const void* rowp, const float* x, const int n, const int dtype) {
+    __m512 b0 = _mm512_setzero_ps(), b1 = _mm512_setzero_ps();  /* [a0 | a1], [a2 | a3] */
+    int j = 0;
+    if (dtype == XH_F16) {
+        const uint16_t* row = (const uint16_t*)rowp;
+        for (; j + 32 <= n; j += 32) {
+            b0 = _mm512_fmadd_ps(_mm512_cvtph_ps(_mm256_loadu_si256((const __m256i*)(row + j))), _mm512_loadu_ps(x + j), b0);
+            b1 = _mm512_fmadd_ps(_mm512_cvtph_ps(_mm256_loadu_si256((const __m256i*)(row + j + 16))), _mm512_loadu_ps(x + j + 16), b1);
+        }
+    } else {
+        const uint8_t* row = (const uint8_t*)rowp;
+        const int e5 = dtype == XH_F8_E5M2;
+        for (; j + 32 <= n; j += 32) {
+            b0 = _mm512_fmadd_ps(f8x16(row + j, e5), _mm512_loadu_ps(x + j), b0);
+            b1 = _mm512_fmadd_ps(f8x16(row + j + 16, e5), _mm512_loadu_ps(x + j + 16), b1);
+        }
+    }
+    /* upper halves through the AVX512F 64x4 extract (the 32x8 one is AVX512DQ) */
+    const __m256 h0 = _mm256_castpd_ps(_mm512_extractf64x4_pd(_mm512_castps_pd(b0), 1));
+    const __m256 h1 = _mm256_castpd_ps(_mm512_extractf64x4_pd(_mm512_castps_pd(b1), 1));
+    float val = hsum8(_mm512_castps512_ps256(b0), h0, _mm512_castps512_ps256(b1), h1);
+    if (dtype == XH_F16) {
+        const uint16_t* row = (const uint16_t*)rowp;
+        for (; j < n; j++) val += xo_f16_to_f32(row[j]) * x[j];
+    } else {
+        const uint8_t* row = (const uint8_t*)rowp;
+        for (; j < n; j++) val += (dtype == XH_F8_E5M2 ? f8e5m2_to_f32(row[j]) : f8e4m3_to_f32(row[j])) * x[j];
+    }
+    return val;
+}
+typedef float (*xo_dot_fn)(const void*, const float*, int, int);
+static xo_dot_fn dot_lanes = 0;
+static int xo_isa_level = -1; /* 1 = AVX2/FMA/F16C, 2 = + AVX-512 */
+static void pick_isa(void) {
+    if (xo_isa_level >= 0) return;
+    __builtin_cpu_init();
+    const int avx512 = __builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512bw") &&
+                       __builtin_cpu_supports("avx512vl") && !(getenv("XO_NO_AVX512") && atoi(getenv("XO_NO_AVX512")));
+    dot_lanes = avx512 ? dot_lanes_avx512 : dot_lanes_avx2;
+    xo_isa_level = avx512 ? 2 : 1;
+}
+int xo_isa(void) {
+    pick_isa();
+    return xo_isa_level;
+}
+#else
+int xo_isa(void) { return 0; }
+#endif
+
 void xo_matmul(float* xout, const float* x, const void* w, const int dtype, const int n, const int d) {
     int i;
     if (scalar_order < 0) xo_matmul_order();
-    if (dtype == XH_F16 && !scalar_order) {
-        const uint16_t* W = (const uint16_t*)w;
-#pragma omp parallel for schedule(static)
-        for (i = 0; i < d; i++) {
-            const uint16_t* row = W + (size_t)i * n;
-            int j = 0;
-            float val = 0.0f;
 #ifdef XO_SIMD
-            __m256 a0 = _mm256_setzero_ps(), a1 = _mm256_setzero_ps();
-            __m256 a2 = _mm256_setzero_ps(), a3 = _mm256_setzero_ps();
-            for (; j + 32 <= n; j += 32) {
-                a0 = _mm256_fmadd_ps(_mm256_cvtph_ps(_mm_loadu_si128((const __m128i*)(row + j))), _mm256_loadu_ps(x + j), a0);
-                a1 = _mm256_fmadd_ps(_mm256_cvtph_ps(_mm_loadu_si128((const __m128i*)(row + j + 8))), _mm256_loadu_ps(x + j + 8), a1);
-                a2 = _mm256_fmadd_ps(_mm256_cvtph_ps(_mm_loadu_si128((const __m128i*)(row + j + 16))), _mm256_loadu_ps(x + j + 16), a2);
-                a3 = _mm256_fmadd_ps(_mm256_cvtph_ps(_mm_loadu_si128((const __m128i*)(row + j + 24))), _mm256_loadu_ps(x + j + 24), a3);
-            }
-            __m256 s = _mm256_add_ps(_mm256_add_ps(a0, a1), _mm256_add_ps(a2, a3));
-            __m128 s4 = _mm_add_ps(_mm256_castps256_ps128(s), _mm256_extractf128_ps(s, 1));
-            s4 = _mm_hadd_ps(s4, s4);
-            s4 = _mm_hadd_ps(s4, s4);
-            val = _mm_cvtss_f32(s4);
-#endif
-            for (; j < n; j++) val += xo_f16_to_f32(row[j]) * x[j];
-            xout[i] = val;
-        }
+    if ((dtype == XH_F16 || dtype == XH_F8_E4M3 || dtype == XH_F8_E5M2) && !scalar_order) {
+        pick_isa();
+        const size_t esz = dtype == XH_F16 ? 2 : 1;
+#pragma omp parallel for schedule(static)
+        for (i = 0; i < d; i++) xout[i] = dot_lanes((const char*)w + (size_t)i * n * esz, x, n, dtype);
         return;
     }
+#endif
 #ifdef XO_SIMD
     if (dtype == XH_F16) {
         /* sequential order: the same left-to-right product + sum as the generic loop below

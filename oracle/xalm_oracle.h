@@ -43,9 +43,11 @@ void xo_reset(xo_model* m);
 
 /* ops (exposed for tests in the reference, src/model.h:286-316) */
 void xo_matmul(float* xout, const float* x, const void* w, int dtype, int n, int d);
-/* f16 in-row summation order: 0 = 8-wide FMA lanes (default), 1 = sequential */
+/* f16 / fp8 in-row summation order: 0 = 8-wide FMA lanes (default), 1 = sequential */
 void xo_set_matmul_order(int order);
 int xo_matmul_order(void);
+/* the lanes order's instruction set, picked at run time: 2 = AVX-512, 1 = AVX2, 0 = scalar */
+int xo_isa(void);
 void xo_rmsnorm(float* o, const float* x, const void* w, int dtype, int size, float eps);
 void xo_rope(float* vec, int d, int head_dim, int pos, float theta, int rotary_dim);
 void xo_mha(float* xout, float* att, const uint16_t* kb, const uint16_t* vb, const float* q,

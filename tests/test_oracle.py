@@ -162,3 +162,42 @@ def test_oracle_f64_evaluation(name, t):
             assert np.all(np.abs(ka - kb) <= np.abs(kb) * 2.0 ** -10 + 2.0 ** -24)
         else:  # after a layer of differently rounded activations: the GPU tests' K/V bar
             assert np.abs(ka - kb).max() <= 2e-3 * max(1.0, float(np.abs(kb).max())), layer
+
+
+_ISA_SCRIPT = r"""
+import sys
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+from oracle import oracle as O
+rng = np.random.default_rng(3)
+out = {}
+for dt in (2, 6, 7):
+    n, d = 4096 + 40, 48
+    if dt == 2:
+        w = rng.standard_normal((d, n)).astype(np.float16).view(np.uint16)
+    else:
+        w = rng.integers(0, 256, (d, n), dtype=np.uint8)
+    x = rng.standard_normal(n).astype(np.float32)
+    o = np.zeros(d, np.float32)
+    O._load().xo_matmul(O._p(o), O._p(x), O._p(np.ascontiguousarray(w)), dt, n, d)
+    out[dt] = o.view(np.uint32).tolist()
+print(O.isa(), out)
+"""
+
+
+def test_lanes_order_same_bits_on_every_isa():
+    """The lanes-order matvec (f16, e4m3, e5m2) picks AVX-512 or AVX2 at run time
+    (-march=native); both forms must give the same bits, so the timed CPU
+    baseline and the parity tests' f32 evaluation are one algorithm on any host."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    runs = []
+    for env_extra in ({}, {"XO_NO_AVX512": "1"}):
+        env = dict(os.environ, **env_extra)
+        r = subprocess.run([sys.executable, "-c", _ISA_SCRIPT, root], capture_output=True, text=True, env=env,
+                           timeout=120, check=True)
+        isa, res = r.stdout.strip().split(" ", 1)
+        runs.append((int(isa), res))
+    assert runs[1][0] == 1
+    assert runs[0][1] == runs[1][1]

@@ -14,9 +14,11 @@ at least as close to that value as the reference's own f32 loop is:
 
 for the batched prompt path, the token-by-token path and the device greedy loop, plus argmax
 agreement with oracle64 wherever its top-2 margin exceeds twice that spread.  Workloads are
-bench.py's (BASELINE configs[1..4]: Mistral-7B f16 4k, fp8 e4m3 with bf16 embed / lm_head,
--T 32768 with a full ring and the StreamingLLM sinks, Llama-3-8B V = 128256), synthetic weights
-generated bit-identically on the device and the host (include/xalm_synth.h).
+bench.py's (BASELINE configs[1..4]: Mistral-7B f16 4k (two weight seeds), fp8 e4m3 with bf16
+embed / lm_head, -T 32768 with a full ring and the StreamingLLM sinks, Llama-3-8B V = 128256; and
+the SURVEY 8f-4 gguf Q8_0 / Q4_0 block workloads, quants.py:281-465), synthetic weights generated
+bit-identically on the device and the host (include/xalm_synth.h).  The 32k ring is also checked
+through a batched prompt pass over a 32700-slot history (test_long_history_prompt_pass).
 """
 import json
 import os
@@ -32,17 +34,17 @@ from xalm_amd.model import InferenceState, Model
 
 pytestmark = [pytest.mark.gpu, pytest.mark.timeout(1200)]
 
-DECODE = 3  # device greedy steps after the prompt (32k: after the one-token hydrate)
+DECODE = 16  # device greedy steps after the prompt (32k: after the one-token hydrate)
 
 
 def maxabs(a, b):
     return float(np.abs(np.asarray(a, np.float64) - np.asarray(b, np.float64)).max())
 
 
-def gpu_side(w, c):
+def gpu_side(w, c, shift=0):
     """GPU logits: batched prompt, token loop, and DECODE device greedy steps after the loop."""
     gm = Model(c)
-    for kind, layer, dt, seed, mean, std in bench.tensor_specs(w):
+    for kind, layer, dt, seed, mean, std in bench.tensor_specs(w, shift):
         gm.upload_synthetic(kind, layer, dt, seed, mean, std)
     prompt = bench.prompt_tokens(c.vocab_size)
     st = InferenceState(c)
@@ -85,8 +87,8 @@ def oracle_side(w, c, g, weights, kv):
     f32 orders; teacher-forced on the GPU's tokens so every variant sees the same inputs."""
     res = {}
     for name, prec, order in (("o64", 1, 0), ("lanes", 0, 0), ("seq", 0, 1)):
-        if name == "seq" and w["wdt"] != L.F16:
-            continue  # the non-f16 matmuls have one (sequential) order only: lanes == seq
+        if name == "seq" and w["wdt"] not in (L.F16, L.F8_E4M3, L.F8_E5M2):
+            continue  # bf16 / gguf matmuls have one (sequential) order only: lanes == seq
         O.set_matmul_order(order)
         om = O.OracleModel(c)
         try:
@@ -110,34 +112,21 @@ def oracle_side(w, c, g, weights, kv):
     return res
 
 
-@pytest.mark.parametrize("workload", ["mistral-7b-f16", "mistral-7b-f8", "llama3-8b-f16", "mistral-7b-f16-32k"])
-def test_full_size_within_reference_f32_error_of_exact(workload):
-    w = bench.WORKLOADS[workload]
-    c = bench.make_config(w)
-    g = gpu_side(w, c)
-    weights = [(kind, layer, dt, O.synthetic(*bench.tensor_shape(c, kind), dt, seed, mean, std))
-               for kind, layer, dt, seed, mean, std in bench.tensor_specs(w)]
-    kv = []
-    if w["kv_prefill"]:
-        kv_dim = c.n_kv_heads * c.head_dim
-        kv = [(layer, which, O.synthetic(w["kv_prefill"], kv_dim, L.F16, 5000 + 2 * layer + which, 0.0, 1.0))
-              for layer in range(c.n_layers) for which in (0, 1)]
-    o = oracle_side(w, c, g, weights, kv)
-    del weights, kv
+def check_report(rep, g, o, checks):
+    """GPU within the reference f32 evaluation's distance from oracle64 on every path, argmax
+    agreement outside near-ties; the report goes to stdout and XALM_PARITY_OUT (jsonl)."""
     exact0, exactN = o["o64"][0], o["o64"][1]
     f32 = [k for k in ("lanes", "seq") if k in o]
     spread0 = max(maxabs(o[k][0], exact0) for k in f32)
     spreadN = max(maxabs(o[k][1], exactN) for k in f32)
-    rep = {"workload": workload, "logit_scale": float(np.abs(exact0).max()),
-           "oracle32_vs_oracle64": {k: [maxabs(o[k][0], exact0), maxabs(o[k][1], exactN)] for k in f32},
-           "gpu_vs_oracle64": {}, "gpu_vs_oracle32_lanes": {},
-           "oracle_seconds": {k: round(v[2], 1) for k, v in o.items()}, "gpu_tokens": g["tokens"]}
-    checks = [("prefill", 0), ("loop", 0), ("decode", 1)]
+    rep.update({"logit_scale": float(np.abs(exact0).max()),
+                "oracle32_vs_oracle64": {k: [maxabs(o[k][0], exact0), maxabs(o[k][1], exactN)] for k in f32},
+                "gpu_vs_oracle64": {}, "gpu_vs_oracle32_lanes": {},
+                "oracle_seconds": {k: round(v[2], 1) for k, v in o.items()}, "gpu_tokens": g.get("tokens", [])})
     for path, idx in checks:
         if path not in g:
             continue
-        e = maxabs(g[path], o["o64"][idx])
-        rep["gpu_vs_oracle64"][path] = e
+        rep["gpu_vs_oracle64"][path] = maxabs(g[path], o["o64"][idx])
         rep["gpu_vs_oracle32_lanes"][path] = maxabs(g[path], o["lanes"][idx])
     print(json.dumps(rep))
     out = os.environ.get("XALM_PARITY_OUT")
@@ -153,5 +142,62 @@ def test_full_size_within_reference_f32_error_of_exact(workload):
         top2 = np.sort(exact)[-2:]
         if top2[1] - top2[0] > 2 * bound:
             assert int(np.argmax(g[path])) == int(np.argmax(exact)), path
+
+
+# (workload, weight seed shift): the BASELINE GPU configs, a second draw of configs[1], and the
+# gguf block workloads (their oracle decodes every block element as quants.py dequantizes it)
+CASES = [("mistral-7b-f16", 0), ("mistral-7b-f16", 7919), ("mistral-7b-f8", 0), ("llama3-8b-f16", 0),
+         ("mistral-7b-f16-32k", 0), ("mistral-7b-q8_0", 0), ("mistral-7b-q4_0", 0)]
+
+
+@pytest.mark.parametrize("workload,shift", CASES, ids=[f"{w}-seed{s}" for w, s in CASES])
+def test_full_size_within_reference_f32_error_of_exact(workload, shift):
+    w = bench.WORKLOADS[workload]
+    c = bench.make_config(w)
+    g = gpu_side(w, c, shift)
+    weights = [(kind, layer, dt, O.synthetic(*bench.tensor_shape(c, kind), dt, seed, mean, std))
+               for kind, layer, dt, seed, mean, std in bench.tensor_specs(w, shift)]
+    kv = []
+    if w["kv_prefill"]:
+        kv_dim = c.n_kv_heads * c.head_dim
+        kv = [(layer, which, O.synthetic(w["kv_prefill"], kv_dim, L.F16, 5000 + 2 * layer + which, 0.0, 1.0))
+              for layer in range(c.n_layers) for which in (0, 1)]
+    o = oracle_side(w, c, g, weights, kv)
+    del weights, kv
+    check_report({"workload": workload, "seed_shift": shift, "decode_steps": DECODE}, g, o,
+                 [("prefill", 0), ("loop", 0), ("decode", 1)])
     # the device greedy tokens: each is oracle64's argmax at its step unless that step is a near-tie
     # (checked through the final logits above; the teacher-forced tokens are the GPU's own)
+
+
+def test_long_history_prompt_pass():
+    """configs[3]'s ring through the batched prompt path: a 32700-slot synthetic history, then one
+    32-token prompt pass at pos0 = 32700 (no wrap: prefill.h's MFMA prompt attention over the whole
+    history, src/infer.cpp:604-638 HYDRATE per token in the reference), logits of its last token;
+    and DECODE device greedy steps after it (the split-KV decode attention at 32.7k slots)."""
+    w = bench.WORKLOADS["mistral-7b-f16-32k"]
+    c = bench.make_config(w)
+    hist, n = 32700, 32
+    prompt = bench.prompt_tokens(c.vocab_size, n=n, seed=13)
+    kv_dim = c.n_kv_heads * c.head_dim
+    gm = Model(c)
+    for kind, layer, dt, seed, mean, std in bench.tensor_specs(w):
+        gm.upload_synthetic(kind, layer, dt, seed, mean, std)
+    for layer in range(c.n_layers):
+        gm.kv_fill_synthetic(layer, 0, 0, hist, 5000 + 2 * layer, 1.0)
+        gm.kv_fill_synthetic(layer, 1, 0, hist, 5001 + 2 * layer, 1.0)
+    st = InferenceState(c)
+    gm.prefill(prompt, hist, st)
+    g = {"prefill": st.logits().copy(), "hydrate": prompt, "pos0": hist}
+    g["tokens"] = list(gm.decode_greedy(hist + n, DECODE))
+    gm.get_logits(st)
+    g["decode"] = st.logits().copy()
+    gm.close()
+    weights = [(kind, layer, dt, O.synthetic(*bench.tensor_shape(c, kind), dt, seed, mean, std))
+               for kind, layer, dt, seed, mean, std in bench.tensor_specs(w)]
+    kv = [(layer, which, O.synthetic(hist, kv_dim, L.F16, 5000 + 2 * layer + which, 0.0, 1.0))
+          for layer in range(c.n_layers) for which in (0, 1)]
+    o = oracle_side(w, c, g, weights, kv)
+    del weights, kv
+    check_report({"workload": "mistral-7b-f16-32k prompt pass", "pos0": hist, "prompt_tokens": n,
+                  "decode_steps": DECODE}, g, o, [("prefill", 0), ("decode", 1)])

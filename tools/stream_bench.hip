@@ -181,7 +181,7 @@ void variant(std::vector<Row>& out, const std::vector<char*>& bufs, unsigned* si
 }
 
 int main(int argc, char** argv) {
-    const int which = argc > 1 ? atoi(argv[1]) : 0;  // 0: W1/W3 policy sweep, 1: per-launch floors
+    const int which = argc > 1 ? atoi(argv[1]) : 0;  // 0: W1/W3 policy sweep, 1: per-launch floors, 2: fp8 pattern sweep
     std::vector<char*> bufs(COPIES);
     for (auto& b : bufs) {
         CK(hipMalloc(&b, BUF));
@@ -213,6 +213,36 @@ int main(int argc, char** argv) {
             variant<256, 2, 4, true, true>(v, bufs, sink, 512, n, rb, s);
             variant<512, 2, 2, true, true>(v, bufs, sink, 512, n, rb, s);
             variant<256, 2, 8, true, true>(v, bufs, sink, 512, n, rb, s);
+        } else if (which == 2) {
+            // one-byte weights: bytes per wave step and rows per wave (W1/W3 pairs need 2 rows)
+            struct Sh { const char* s; int n, rb; };
+            const Sh f8[] = {{"w13 f8", 28672, 4096}, {"qkv f8", 6144, 4096}};
+            for (const Sh& h : f8) {
+                variant<512, 2, 4, true, false>(v, bufs, sink, 448, h.n, h.rb, h.s);
+                variant<512, 2, 1, true, false>(v, bufs, sink, 448, h.n, h.rb, h.s);
+                variant<512, 2, 1, true, false>(v, bufs, sink, 256, h.n, h.rb, h.s);
+                variant<512, 2, 1, true, false>(v, bufs, sink, 512, h.n, h.rb, h.s);
+                variant<512, 2, 1, true, false>(v, bufs, sink, 1024, h.n, h.rb, h.s);
+                variant<256, 2, 1, true, false>(v, bufs, sink, 1024, h.n, h.rb, h.s);
+                variant<1024, 2, 1, true, false>(v, bufs, sink, 256, h.n, h.rb, h.s);
+                variant<512, 1, 1, true, false>(v, bufs, sink, 512, h.n, h.rb, h.s);
+                variant<512, 1, 2, true, false>(v, bufs, sink, 512, h.n, h.rb, h.s);
+                variant<512, 1, 4, true, false>(v, bufs, sink, 512, h.n, h.rb, h.s);
+                variant<512, 2, 2, true, false>(v, bufs, sink, 256, h.n, h.rb, h.s);
+                variant<384, 2, 4, true, false>(v, bufs, sink, 512, h.n, h.rb, h.s);
+                variant<384, 2, 1, true, false>(v, bufs, sink, 512, h.n, h.rb, h.s);
+            }
+            const Sh f16[] = {{"w13 f16", 28672, 8192}, {"qkv f16", 6144, 8192}, {"w2 f16", 4096, 28672}};
+            for (const Sh& h : f16) {
+                variant<512, 2, 4, true, false>(v, bufs, sink, 448, h.n, h.rb, h.s);
+                variant<512, 2, 2, true, false>(v, bufs, sink, 448, h.n, h.rb, h.s);
+                variant<512, 2, 1, true, false>(v, bufs, sink, 448, h.n, h.rb, h.s);
+                variant<512, 2, 2, true, false>(v, bufs, sink, 256, h.n, h.rb, h.s);
+                variant<512, 1, 2, true, false>(v, bufs, sink, 512, h.n, h.rb, h.s);
+                variant<512, 1, 4, true, false>(v, bufs, sink, 256, h.n, h.rb, h.s);
+                variant<384, 2, 4, true, false>(v, bufs, sink, 512, h.n, h.rb, h.s);
+                variant<1024, 1, 4, true, false>(v, bufs, sink, 256, h.n, h.rb, h.s);
+            }
         } else {
             // the decode launches' matrices (Mistral-7B), f16 and fp8, at 8 and 16 waves per CU
             struct Sh { const char* s; int n, rb; };
