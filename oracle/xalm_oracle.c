@@ -339,8 +339,13 @@ void xo_matmul(float* xout, const float* x, const void* w, const int dtype, cons
 #pragma omp parallel for schedule(static)
             for (i = 0; i < d; i++) {
                 const uint8_t* row = (const uint8_t*)w + (size_t)i * nb * bs;
-                float val = 0.0f;
-                for (int j = 0; j < n; j++) val += xo_gq_elem(dtype, row + (size_t)(j / 32) * bs, j % 32) * x[j];
+                float val = 0.0f, f[32];
+                for (size_t b = 0; b < nb; b++) {  /* one block's 32 values, then the same sums in j order */
+                    const uint8_t* blk = row + b * bs;
+                    for (int k = 0; k < 32; k++) f[k] = xo_gq_elem(dtype, blk, k);
+                    const float* xb = x + b * 32;
+                    for (int k = 0; k < 32; k++) val += f[k] * xb[k];
+                }
                 xout[i] = val;
             }
             break;
@@ -397,6 +402,14 @@ void xo_rope(float* vec, const int d, const int head_dim, const int pos, const f
     }
 }
 
+/* f16 -> f32 in the attention loops: F16C's conversion is exact and equal to xo_f16_to_f32 for
+ * every non-NaN code (a NaN stays a NaN, its payload may differ) */
+#ifdef XO_SIMD
+static inline float f16f(const uint16_t h) { return _cvtsh_ss(h); }
+#else
+static inline float f16f(const uint16_t h) { return xo_f16_to_f32(h); }
+#endif
+
 /* attn, src/infer.cpp:325-359: one head over kv_len ring slots in slot order. */
 static void attn(float* xout, float* atth, const float* qh, const uint16_t* kh, const uint16_t* vh,
                  const int head_dim, const int n_kv_heads, const int kv_len) {
@@ -404,15 +417,22 @@ static void attn(float* xout, float* atth, const float* qh, const uint16_t* kh, 
     const float sqrt_head_dim = 1.0f / sqrtf((float)head_dim);
     for (int t = 0; t < kv_len; ++t) {
         float score = 0.0f;
-        for (int i = 0; i < head_dim; ++i) score += qh[i] * xo_f16_to_f32(kh[(size_t)t * kv_stride + i]);
+        for (int i = 0; i < head_dim; ++i) score += qh[i] * f16f(kh[(size_t)t * kv_stride + i]);
         atth[t] = score * sqrt_head_dim;
     }
     softmax(atth, atth, kv_len);
-    for (int i = 0; i < head_dim; ++i) {
-        float vi = 0.0f;
-        for (int t = 0; t < kv_len; ++t) vi += atth[t] * xo_f16_to_f32(vh[(size_t)t * kv_stride + i]);
-        xout[i] = vi;
+    /* xout[i] = sum over t in slot order of atth[t] * v[t][i] (src/infer.cpp:349-356), with the
+     * loops interchanged so V is read row by row: every xout[i] still receives its terms in slot
+     * order, so the sums are the same bits as the column-major loop (which re-walks the whole
+     * ring once per dimension: ~100x slower at 32k slots) */
+    float vacc[512];
+    for (int i = 0; i < head_dim; ++i) vacc[i] = 0.0f;
+    for (int t = 0; t < kv_len; ++t) {
+        const uint16_t* vr = vh + (size_t)t * kv_stride;
+        const float a = atth[t];
+        for (int i = 0; i < head_dim; ++i) vacc[i] += a * f16f(vr[i]);
     }
+    for (int i = 0; i < head_dim; ++i) xout[i] = vacc[i];
 }
 
 /* mha_cpu, src/infer.cpp:498-517 */
@@ -476,6 +496,7 @@ struct xo_model {
 static void* xcalloc(size_t n, size_t sz) { return calloc(n ? n : 1, sz); }
 
 xo_model* xo_create(const xh_config* cfg) {
+    if (cfg->head_dim <= 0 || cfg->head_dim > 512) return NULL; /* attn's row accumulators hold 512 */
     xo_model* m = (xo_model*)xcalloc(1, sizeof(xo_model));
     if (!m) return NULL;
     m->c = *cfg;
@@ -718,6 +739,22 @@ static void matmul64(double* xout, const double* x, const void* w, const int dty
         }
         return;
     }
+    if (xo_gq(dtype)) {
+        /* gguf blocks: each block's 32 values decoded once, then the same sums in j order */
+        const size_t nb = (size_t)n / 32, bs = xo_gq_bs(dtype);
+#pragma omp parallel for schedule(static)
+        for (i = 0; i < d; i++) {
+            const uint8_t* row = (const uint8_t*)w + (size_t)i * nb * bs;
+            double val = 0.0;
+            float f[32];
+            for (size_t b = 0; b < nb; b++) {
+                for (int k = 0; k < 32; k++) f[k] = xo_gq_elem(dtype, row + b * bs, k);
+                for (int k = 0; k < 32; k++) val += (double)f[k] * x[b * 32 + k];
+            }
+            xout[i] = val;
+        }
+        return;
+    }
 #pragma omp parallel for schedule(static)
     for (i = 0; i < d; i++) {
         double val = 0.0;
@@ -758,7 +795,7 @@ static void attn64(double* xout, double* atth, const double* qh, const uint16_t*
     double mx = -DBL_MAX;
     for (int t = 0; t < kv_len; ++t) {
         double score = 0.0;
-        for (int i = 0; i < head_dim; ++i) score += qh[i] * (double)xo_f16_to_f32(kh[(size_t)t * kv_stride + i]);
+        for (int i = 0; i < head_dim; ++i) score += qh[i] * (double)f16f(kh[(size_t)t * kv_stride + i]);
         atth[t] = score * inv_sqrt;
         if (atth[t] > mx) mx = atth[t];
     }
@@ -768,11 +805,14 @@ static void attn64(double* xout, double* atth, const double* qh, const uint16_t*
         sum += atth[t];
     }
     for (int t = 0; t < kv_len; ++t) atth[t] /= sum;
-    for (int i = 0; i < head_dim; ++i) {
-        double vi = 0.0;
-        for (int t = 0; t < kv_len; ++t) vi += atth[t] * (double)xo_f16_to_f32(vh[(size_t)t * kv_stride + i]);
-        xout[i] = vi;
+    double vacc[512];  /* row-major V walk, each sum in slot order (as attn) */
+    for (int i = 0; i < head_dim; ++i) vacc[i] = 0.0;
+    for (int t = 0; t < kv_len; ++t) {
+        const uint16_t* vr = vh + (size_t)t * kv_stride;
+        const double a = atth[t];
+        for (int i = 0; i < head_dim; ++i) vacc[i] += a * (double)f16f(vr[i]);
     }
+    for (int i = 0; i < head_dim; ++i) xout[i] = vacc[i];
 }
 
 static inline double clip64(const double x, const double v) { return x < -v ? -v : (x > v ? v : x); }
