@@ -4,7 +4,7 @@
 # Each GPU step has its own limit; a crash / abort / timeout ends the run.
 set -u
 cd "$(dirname "$0")/.."
-ROUND=${ROUND:-r04}
+ROUND=${ROUND:-r05}
 PART=${PART:-all}   # a: tests, PMC, kernel trace, fp16 / fp8 benches; b: the other workloads
 OUT=gpurun_out/$ROUND
 mkdir -p "$OUT"
@@ -19,8 +19,10 @@ step() {
     if [ $rc -ne 0 ]; then tail -5 "$OUT/$name.log"; exit $rc; fi
 }
 if [ "$PART" != b ]; then
+if [ -z "${SKIP_TESTS:-}" ]; then
 step smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()"
-step pytest_gpu 900 python3 -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread -rs
+step pytest_gpu 900 python3 -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread -rs
+fi
 # HBM traffic (MI355X_MICROARCH.md HBM section): FETCH_SIZE and WRITE_SIZE in separate passes
 for c in FETCH_SIZE WRITE_SIZE; do
     step pmc_$c 300 rocprofv3 --pmc $c --kernel-trace -d "$OUT/pmc/$c" -o run --output-format csv -- \
@@ -43,12 +45,21 @@ step bench 600 python3 bench.py
 step bench_f8 600 python3 bench.py --workload mistral-7b-f8
 fi
 if [ "$PART" != a ]; then
+step kernel_trace_32k 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_32k" -o run --output-format csv -- \
+    python3 bench.py --workload mistral-7b-f16-32k --steps 32 --warmup 4 --no-cpu-baseline --kernel-iters 20 --prefill-tokens 0
+cp "$OUT/prof_32k/run_kernel_stats.csv" "$OUT/kernel_stats_32k.csv"
+step kernel_trace_llama 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_llama" -o run --output-format csv -- \
+    python3 bench.py --workload llama3-8b-f16 --steps 64 --warmup 4 --no-cpu-baseline --kernel-iters 50 --prefill-tokens 0
+cp "$OUT/prof_llama/run_kernel_stats.csv" "$OUT/kernel_stats_llama.csv"
+step kernel_trace_q4_0 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_q4" -o run --output-format csv -- \
+    python3 bench.py --workload mistral-7b-q4_0 --steps 64 --warmup 4 --no-cpu-baseline --kernel-iters 50 --prefill-tokens 0
+cp "$OUT/prof_q4/run_kernel_stats.csv" "$OUT/kernel_stats_q4_0.csv"
 step bench_32k 900 python3 bench.py --workload mistral-7b-f16-32k --steps 64 --cpu-tokens 8
 step bench_llama 600 python3 bench.py --workload llama3-8b-f16
-# SURVEY 8f-4 block formats (not BASELINE configs; the oracle's per-element block decode makes
-# a CPU sample slow, so none)
-step bench_q8_0 600 python3 bench.py --workload mistral-7b-q8_0 --no-cpu-baseline
-step bench_q4_0 600 python3 bench.py --workload mistral-7b-q4_0 --no-cpu-baseline
+# SURVEY 8f-4 block formats (not BASELINE configs): a shorter CPU sample (the oracle decodes
+# every block element as quants.py does)
+step bench_q8_0 600 python3 bench.py --workload mistral-7b-q8_0 --cpu-tokens 16
+step bench_q4_0 600 python3 bench.py --workload mistral-7b-q4_0 --cpu-tokens 16
 fi
 for b in bench bench_f8 bench_32k bench_llama bench_q8_0 bench_q4_0; do [ -f "$OUT/$b.log" ] && tail -1 "$OUT/$b.log" > "$OUT/$b.json"; done
 echo "== done"
