@@ -165,6 +165,53 @@ double time_us(F launch, const std::vector<char*>& bufs, int iters) {
 
 struct Row { std::string name; double bytes; double us; };
 
+// K/V ring of one layer at 32k slots (rows of 2 KiB = 8 KV heads x 256 B), K then V, register
+// loads, nt, two rounds of 4 x 16 B per thread in flight.
+//   HEADS = 1: workgroup (KV head b % 8, split b / 8) reads its 256-B slice of each of its rows
+//              (the decode attention's split layout)
+//   HEADS = 8: workgroup (split b) reads whole 2-KiB rows (every KV head of a slot range)
+template <int HEADS, int THREADS>
+__global__ __launch_bounds__(THREADS) void kv_kernel(const char* kc, const char* vc, const int rows_per_wg, unsigned* sink) {
+    const int tid = threadIdx.x;
+    constexpr int LPR = 16 * HEADS;       // lanes per row
+    constexpr int RPP = THREADS / LPR;    // rows per pass
+    const int g = HEADS == 1 ? blockIdx.x % 8 : 0;
+    const int split = HEADS == 1 ? blockIdx.x / 8 : blockIdx.x;
+    const size_t row0 = (size_t)split * rows_per_wg;
+    const int sub = tid % LPR, rr = tid / LPR;
+    uint32_t acc = 0;
+    const int rounds = rows_per_wg / (4 * RPP);
+    for (int which = 0; which < 2; which++) {
+        const char* base = (which ? vc : kc) + row0 * 2048 + g * 256 + sub * 16;
+        u4 cur[4], nxt[4];
+        auto load = [&](u4 (&v)[4], int r) {
+#pragma unroll
+            for (int p = 0; p < 4; p++)
+                v[p] = __builtin_nontemporal_load((gp4)(base + ((size_t)r * 4 * RPP + p * RPP + rr) * 2048));
+        };
+        load(cur, 0);
+        for (int r = 0; r < rounds; r++) {
+            if (r + 1 < rounds) load(nxt, r + 1);
+#pragma unroll
+            for (int p = 0; p < 4; p++) acc ^= cur[p].x ^ cur[p].y;
+#pragma unroll
+            for (int p = 0; p < 4; p++) cur[p] = nxt[p];
+        }
+    }
+    if (acc == 0x12345678u) sink[blockIdx.x] = acc;
+}
+
+template <int HEADS, int THREADS>
+void kv_variant(std::vector<Row>& out, const std::vector<char*>& bufs, unsigned* sink, int nwg, const char* name) {
+    constexpr size_t RING = 32768ull * 2048;  // one layer's K (or V)
+    const int rows_per_wg = (int)(32768ull * (HEADS == 1 ? 8 : 1) / nwg);
+    auto launch = [&](char* b) {
+        hipLaunchKernelGGL((kv_kernel<HEADS, THREADS>), dim3(nwg), dim3(THREADS), 0, 0, b, b + RING, rows_per_wg, sink);
+    };
+    out.push_back({name, 2.0 * RING, time_us(launch, bufs, 32)});
+}
+
+
 template <int THREADS, int ROWS, int U, bool NT, bool LDS>
 void variant(std::vector<Row>& out, const std::vector<char*>& bufs, unsigned* sink, int blocks, int nrows, int row_bytes,
              const char* shape) {
@@ -213,6 +260,14 @@ int main(int argc, char** argv) {
             variant<256, 2, 4, true, true>(v, bufs, sink, 512, n, rb, s);
             variant<512, 2, 2, true, true>(v, bufs, sink, 512, n, rb, s);
             variant<256, 2, 8, true, true>(v, bufs, sink, 512, n, rb, s);
+        } else if (which == 3) {
+            kv_variant<1, 1024>(v, bufs, sink, 256, "kv 256-B head slices  256 wg x 1024t");
+            kv_variant<1, 1024>(v, bufs, sink, 512, "kv 256-B head slices  512 wg x 1024t");
+            kv_variant<1, 512>(v, bufs, sink, 512, "kv 256-B head slices  512 wg x  512t");
+            kv_variant<8, 1024>(v, bufs, sink, 256, "kv 2-KiB rows          256 wg x 1024t");
+            kv_variant<8, 1024>(v, bufs, sink, 512, "kv 2-KiB rows          512 wg x 1024t");
+            kv_variant<8, 512>(v, bufs, sink, 512, "kv 2-KiB rows          512 wg x  512t");
+            kv_variant<8, 512>(v, bufs, sink, 1024, "kv 2-KiB rows         1024 wg x  512t");
         } else if (which == 2) {
             // one-byte weights: bytes per wave step and rows per wave (W1/W3 pairs need 2 rows)
             struct Sh { const char* s; int n, rb; };
