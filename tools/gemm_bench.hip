@@ -86,11 +86,16 @@ int main(int argc, char** argv) {
     const size_t wss = 256ull << 20;
     CK(hipMalloc(&ws, wss));
     CK(hipMemcpy(dw, hw.data(), wmax * 2, hipMemcpyHostToDevice));
-    struct Var { const char* name; void (*fn)(xalm::MmArgs); int lds; int bt; };
+    struct Var { const char* name; void (*fn)(xalm::MmArgs); int lds; int bt; int threads = xalm::MM_THREADS; };
     const Var vars[] = {
         {"m16g", xalm::mm_f16_kernel_t<64, 2, 12, 128>, xalm::MmCfg<64, 2, 128>::LDS, 128},
         {"m16b32s3", xalm::mm_f16_kernel_t<32, 3, 12, 128>, xalm::MmCfg<32, 3, 128>::LDS, 128},
         {"m16b32o4", xalm::mm_f16_kernel_t<32, 2, 12, 128, 4>, xalm::MmCfg<32, 2, 128>::LDS, 128},
+        // 4 waves: each wave 64 tokens x 128 rows (a third less LDS read per MFMA)
+        {"w4b64", xalm::mm_f16_kernel_t<64, 2, 12, 128, 1, 4>, xalm::MmCfg<64, 2, 128, 4>::LDS, 128, 256},
+        {"w4b32s4", xalm::mm_f16_kernel_t<32, 4, 12, 128, 1, 4>, xalm::MmCfg<32, 4, 128, 4>::LDS, 128, 256},
+        {"w4b32o2", xalm::mm_f16_kernel_t<32, 2, 12, 128, 2, 4>, xalm::MmCfg<32, 2, 128, 4>::LDS, 128, 256},
+        {"w4b64p", xalm::mm_f16_kernel_t<64, 2, 13, 128, 1, 4>, xalm::MmCfg<64, 2, 128, 4>::LDS, 128, 256},
     };
     const int NV = sizeof vars / sizeof vars[0];
     for (int v = 0; v < NV; v++)
@@ -130,7 +135,7 @@ int main(int argc, char** argv) {
                 a.ks = xalm::mm_pick_ks(sh.rows, sh.K, n, (size_t)2 * 2048 * 28672, 256, vars[v].bt);
                 grid = a.n_rt * a.n_tt * a.ks;
                 auto launch = [&]() {
-                    hipLaunchKernelGGL(vars[v].fn, dim3(grid), dim3(xalm::MM_THREADS), vars[v].lds, 0, a);
+                    hipLaunchKernelGGL(vars[v].fn, dim3(grid), dim3(vars[v].threads), vars[v].lds, 0, a);
                 };
                 CK(hipMemset(dy, 0, (size_t)a.ks * n * sh.rows * 4));
                 launch();

@@ -91,22 +91,23 @@ __device__ __forceinline__ void mm_wait_vm() {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <int BK, int NS, int BT = 128>
+template <int BK, int NS, int BT = 128, int NW = 8>
 struct MmCfg {
     static constexpr int RB = BK * 2;             // LDS image row bytes
     static constexpr int CH = RB / 16;            // 16-B chunks per row
     static constexpr int RPI = 1024 / RB;         // image rows per DMA wave-instruction
     static constexpr int SH = CH == 8 ? 1 : 2;    // swizzle f(r) = (r >> SH) & (CH - 1)
     static constexpr int STAGE = (MM_BR + 2 * BT) * RB;
-    static constexpr int WI = MM_BR / RPI / 8;    // W instructions per wave per stage
-    static constexpr int XI = BT / RPI / 8;       // Xh (and Xl) instructions per wave per stage
+    static constexpr int WI = MM_BR / RPI / NW;   // W instructions per wave per stage
+    static constexpr int XI = BT / RPI / NW;      // Xh (and Xl) instructions per wave per stage
     static constexpr int LPS = WI + 2 * XI;       // DMA instructions per wave per stage
     static constexpr int LDS = NS * STAGE;
     static constexpr int WT = BT / 64;            // waves along the tokens (64 tokens each)
-    static constexpr int WR = 8 / WT;             // waves along the rows
+    static constexpr int WR = NW / WT;            // waves along the rows
     static constexpr int RT = MM_BR / WR / 32;    // 32-row tiles per wave
     static_assert(BK == 32 || BK == 64, "BK");
     static_assert(BT == 128 || BT == 256, "BT");
+    static_assert((NW == 8 || NW == 4) && XI >= 1 && WR >= 1, "NW");
     static_assert(NS >= 2 && LDS <= 160 * 1024, "stages");
     __device__ static uint32_t off(const int r, const int c) { return (uint32_t)(r * RB + 16 * (c ^ ((r >> SH) & (CH - 1)))); }
 };
@@ -125,9 +126,9 @@ __device__ __forceinline__ void mm_wait_ahead(const int ahead) {
 // fastest: the 32 workgroups an XCD runs at once cover 8 x 4 tiles, sharing both operands in L2)
 // OCC: waves per SIMD the register allocation must allow (2: one 512-thread workgroup per CU;
 // 4: two, each with at most 80 KiB of LDS)
-template <int BK, int NS, int FL, int BT = 128, int OCC = 2>
-__global__ __launch_bounds__(MM_THREADS, OCC) void mm_f16_kernel_t(const MmArgs a) {
-    using C = MmCfg<BK, NS, BT>;
+template <int BK, int NS, int FL, int BT = 128, int OCC = 2, int NW = 8>
+__global__ __launch_bounds__(64 * NW, OCC) void mm_f16_kernel_t(const MmArgs a) {
+    using C = MmCfg<BK, NS, BT, NW>;
     extern __shared__ __attribute__((aligned(16))) char mm_smem[];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int h = lane >> 5, l32 = lane & 31;
@@ -205,8 +206,45 @@ __global__ __launch_bounds__(MM_THREADS, OCC) void mm_f16_kernel_t(const MmArgs 
         for (int i = 0; i < 4; i++)
 #pragma unroll
             for (int j = 0; j < RS; j++) acc4[i][j] = mm_f32x4{};
+        struct F16 { mm_f16x8 ah[4], al[4], bw[RS]; };
+        auto load16 = [&](const char* base, const int q, F16& f) {
+            const char* w_img = base;
+            const char* xh_img = base + MM_BR * C::RB;
+            const char* xl_img = base + (MM_BR + BT) * C::RB;
+            const int c = 4 * q + q4;
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const uint32_t o = C::off(64 * wt + 16 * i + l16, c);
+                f.ah[i] = *(const mm_f16x8*)(xh_img + o);
+                f.al[i] = *(const mm_f16x8*)(xl_img + o);
+            }
+#pragma unroll
+            for (int j = 0; j < RS; j++) f.bw[j] = *(const mm_f16x8*)(w_img + C::off(32 * RT * wr + 16 * j + l16, c));
+        };
+        auto mma16 = [&](const F16& f) {
+            if constexpr (FL & 2) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+#pragma unroll
+                for (int j = 0; j < RS; j++) {
+                    acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(f.ah[i], f.bw[j], acc4[i][j], 0, 0, 0);
+                    acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(f.al[i], f.bw[j], acc4[i][j], 0, 0, 0);
+                }
+            if constexpr (FL & 2) __builtin_amdgcn_s_setprio(0);
+        };
         auto compute16 = [&](const int stage) {
             const char* base = mm_smem + stage * C::STAGE;
+            if constexpr (FL & 1) {
+                // the next 32-deep step's fragments requested before this one's MFMAs
+                F16 f0, f1;
+                load16(base, 0, f0);
+#pragma unroll
+                for (int q = 0; q < BK / 32; q++) {
+                    if (q + 1 < BK / 32) load16(base, q + 1, (q & 1) ? f0 : f1);
+                    mma16((q & 1) ? f1 : f0);
+                }
+                return;
+            }
             const char* w_img = base;
             const char* xh_img = base + MM_BR * C::RB;
             const char* xl_img = base + (MM_BR + BT) * C::RB;
