@@ -125,7 +125,8 @@ __device__ __forceinline__ void mm_wait_ahead(const int ahead) {
 // the MFMA clusters; bit 3: 16x16x32 MFMA tiles (BK 64); bit 2: grouped tile order (8 row tiles x n_tt token tiles per group, row tile
 // fastest: the 32 workgroups an XCD runs at once cover 8 x 4 tiles, sharing both operands in L2)
 // OCC: waves per SIMD the register allocation must allow (2: one 512-thread workgroup per CU;
-// 4: two, each with at most 80 KiB of LDS)
+// 4: two, each with at most 80 KiB of LDS).  NW: waves per workgroup, 8 (2 x 4 waves of 64 x 64)
+// or 4 (2 x 2 waves of 64 tokens x 128 rows: a third less LDS read per MFMA)
 template <int BK, int NS, int FL, int BT = 128, int OCC = 2, int NW = 8>
 __global__ __launch_bounds__(64 * NW, OCC) void mm_f16_kernel_t(const MmArgs a) {
     using C = MmCfg<BK, NS, BT, NW>;
@@ -379,7 +380,15 @@ __global__ __launch_bounds__(64 * NW, OCC) void mm_f16_kernel_t(const MmArgs a) 
     }
 }
 
-// the product's instantiation
+// the product's instantiations: the default, and for launches of >= MM_W4_PER_CU workgroups per
+// CU (W1/W3 and the lm_head at 2048 tokens) two 4-wave workgroups per CU with 32-deep steps in
+// 64 KiB each, every wave 64 tokens x 128 rows (tools/gemm_bench, 2048 tokens: W1/W3 840 -> 809
+// us; qkv, Wo, W2 slower, their launches have 1-3 workgroups per CU).  Same k order per
+// accumulator (32-deep MFMA steps, hi then lo), so the same bits as the default.
 #define mm_f16_kernel mm_f16_kernel_t<MM_BK, MM_NS, MM_FL, MM_BT>
+#define mm_f16_kernel_w4 mm_f16_kernel_t<32, 2, MM_FL, MM_BT, 2, 4>
+constexpr int MM_LDS_W4 = MmCfg<32, 2, MM_BT, 4>::LDS;
+constexpr int MM_THREADS_W4 = 256;
+constexpr int MM_W4_PER_CU = 4;
 
 }  // namespace xalm

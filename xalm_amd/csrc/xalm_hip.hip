@@ -970,6 +970,18 @@ void pf_norm(xh_ctx* ctx, const void* nw, int ndt, int m, int dt, int rows) {
                            nw, ndt, c.norm_eps, ctx->pf_xn);
     }
 }
+// one prompt GEMM launch (gemm16.h): the 4-wave instantiation when the launch has at least
+// MM_W4_PER_CU workgroups per CU, else the default
+void mm_launch(const MmArgs& a, int n_cu, hipStream_t s) {
+    const int grid = a.n_rt * a.n_tt * a.ks;
+    if (grid >= MM_W4_PER_CU * n_cu) {
+        ensure_lds((const void*)mm_f16_kernel_w4, MM_LDS_W4);
+        hipLaunchKernelGGL(mm_f16_kernel_w4, dim3(grid), dim3(MM_THREADS_W4), MM_LDS_W4, s, a);
+    } else {
+        ensure_lds((const void*)mm_f16_kernel, MM_LDS);
+        hipLaunchKernelGGL(mm_f16_kernel, dim3(grid), dim3(MM_THREADS), MM_LDS, s, a);
+    }
+}
 // Y partials of W[rows][K] . X[n][K] into pf_part ([ks][n][rows]).  Split-f16 paths convert x
 // first unless pf_norm / the fused GLU already left its halves.  0 or an error code.
 int pf_gemm(xh_ctx* ctx, const char* what, int dt, const void* w, int K, int rows, const float* x, int n, int& ks) {
@@ -1037,12 +1049,11 @@ int pf_gemm(xh_ctx* ctx, const char* what, int dt, const void* w, int K, int row
         a.n_rt = mm_row_tiles(rows); a.n_tt = mm_tok_tiles(n);
         if (a.ks <= 0 || (size_t)images * a.ks * n * rows > cap)
             return set_err(ctx, XH_E_INVALID, "prefill: %s GEMM %d x %d over %d tokens does not fit", what, rows, K, n);
-        ensure_lds((const void*)mm_f16_kernel, MM_LDS);
-        hipLaunchKernelGGL(mm_f16_kernel, dim3(a.n_rt * a.n_tt * a.ks), dim3(MM_THREADS), MM_LDS, ctx->stream, a);
+        mm_launch(a, ctx->n_cu, ctx->stream);
         if (w_lo) {  // partials [ks, 2 ks): W_lo . X, summed after W_hi's by the epilogue
             a.w = w_lo;
             a.out = ctx->pf_part + (size_t)a.ks * n * rows;
-            hipLaunchKernelGGL(mm_f16_kernel, dim3(a.n_rt * a.n_tt * a.ks), dim3(MM_THREADS), MM_LDS, ctx->stream, a);
+            mm_launch(a, ctx->n_cu, ctx->stream);
         }
         ks = images * a.ks;
         return 0;
@@ -2146,8 +2157,10 @@ int xh_op_prompt_gemm(float* y, const uint16_t* w, const uint16_t* xh, const uin
     MmArgs a{};
     a.w = (const uint16_t*)bw.p; a.xh = (const uint16_t*)bx.p; a.xl = (const uint16_t*)bx.p + xe; a.out = (float*)bo.p;
     a.rows = rows; a.K = K; a.n = n; a.ks = ks; a.n_rt = mm_row_tiles(rows); a.n_tt = mm_tok_tiles(n);
-    ensure_lds((const void*)mm_f16_kernel, MM_LDS);
-    hipLaunchKernelGGL(mm_f16_kernel, dim3(a.n_rt * a.n_tt * ks), dim3(MM_THREADS), MM_LDS, nullptr, a);
+    int dev = 0, n_cu = 256;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        return set_err(nullptr, XH_E_HIP, "no device");
+    mm_launch(a, n_cu, nullptr);
     std::vector<float> part((size_t)ks * n * rows);
     if ((rc = op_finish(part.data(), bo, part.size() * 4))) return rc;
     for (size_t i = 0; i < (size_t)n * rows; i++) {
