@@ -170,6 +170,29 @@ def test_full_size_within_reference_f32_error_of_exact(workload, shift):
     # (checked through the final logits above; the teacher-forced tokens are the GPU's own)
 
 
+@pytest.mark.parametrize("workload", ["mistral-7b-f16", "mistral-7b-f8"])
+def test_full_size_2048_token_pass_glu_epilogues_agree(workload):
+    """A 2048-token prompt pass at Mistral-7B shapes (the W1/W3 GEMM on the 4-wave launch):
+    act(g) * u (src/infer.cpp:468-488) fused with the W2 input split (prefill_glu_split_kernel)
+    gives the same logits, bit for bit, as the GLU epilogue kernel + separate split
+    (XH_OPT_PREFILL_GLU_SPLIT 0)."""
+    w = bench.WORKLOADS[workload]
+    c = bench.make_config(w)
+    gm = Model(c)
+    for kind, layer, dt, seed, mean, std in bench.tensor_specs(w):
+        gm.upload_synthetic(kind, layer, dt, seed, mean, std)
+    prompt = bench.prompt_tokens(c.vocab_size, n=2048, seed=11)
+    st = InferenceState(c)
+    got = {}
+    for glu in (1, 0):
+        gm.reset()
+        gm.set_option(L.OPT_PREFILL_GLU_SPLIT, glu)
+        gm.prefill(prompt, 0, st)
+        got[glu] = st.logits().copy()
+    assert np.isfinite(got[1]).all()
+    assert np.array_equal(got[1].view(np.uint32), got[0].view(np.uint32))
+
+
 # configs[3]'s ring through the batched prompt path, in three tests (each well under the runner's
 # silence limit; pytest -x runs them in order and they share _P32): a 32700-slot synthetic history,
 # one 32-token prompt pass at pos0 = 32700 (no wrap: prefill.h's MFMA prompt attention over the

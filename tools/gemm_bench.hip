@@ -86,7 +86,7 @@ int main(int argc, char** argv) {
     const size_t wss = 256ull << 20;
     CK(hipMalloc(&ws, wss));
     CK(hipMemcpy(dw, hw.data(), wmax * 2, hipMemcpyHostToDevice));
-    struct Var { const char* name; void (*fn)(xalm::MmArgs); int lds; int bt; int threads = xalm::MM_THREADS; };
+    struct Var { const char* name; void (*fn)(xalm::MmArgs); int lds; int bt; int threads = xalm::MM_THREADS; int kmul = 1; };
     const Var vars[] = {
         {"m16g", xalm::mm_f16_kernel_t<64, 2, 12, 128>, xalm::MmCfg<64, 2, 128>::LDS, 128},
         {"m16b32s3", xalm::mm_f16_kernel_t<32, 3, 12, 128>, xalm::MmCfg<32, 3, 128>::LDS, 128},
@@ -96,6 +96,10 @@ int main(int argc, char** argv) {
         {"w4b32s4", xalm::mm_f16_kernel_t<32, 4, 12, 128, 1, 4>, xalm::MmCfg<32, 4, 128, 4>::LDS, 128, 256},
         {"w4b32o2", xalm::mm_f16_kernel_t<32, 2, 12, 128, 2, 4>, xalm::MmCfg<32, 2, 128, 4>::LDS, 128, 256},
         {"w4b64p", xalm::mm_f16_kernel_t<64, 2, 13, 128, 1, 4>, xalm::MmCfg<64, 2, 128, 4>::LDS, 128, 256},
+        // the same with twice / four times the K slices of mm_pick_ks (more workgroups per CU)
+        {"w4o2k2", xalm::mm_f16_kernel_t<32, 2, 12, 128, 2, 4>, xalm::MmCfg<32, 2, 128, 4>::LDS, 128, 256, 2},
+        {"w4o2k4", xalm::mm_f16_kernel_t<32, 2, 12, 128, 2, 4>, xalm::MmCfg<32, 2, 128, 4>::LDS, 128, 256, 4},
+        {"m16gk2", xalm::mm_f16_kernel_t<64, 2, 12, 128>, xalm::MmCfg<64, 2, 128>::LDS, 128, 512, 2},
     };
     const int NV = sizeof vars / sizeof vars[0];
     for (int v = 0; v < NV; v++)
@@ -107,7 +111,7 @@ int main(int argc, char** argv) {
     CK(hipEventCreate(&e1));
     int bad = 0;
     for (int n : ns) {
-        double tot_us[8] = {}, tot_bl = 0, tot_flop = 0;
+        double tot_us[16] = {}, tot_bl = 0, tot_flop = 0;
         for (const Shape& sh : shapes) {
             // Xh rows [n][K] then Xl rows [n][K] (the product's layout)
             std::vector<uint16_t> xs(2 * (size_t)n * sh.K);
@@ -132,7 +136,8 @@ int main(int argc, char** argv) {
             for (int v = 0; v < NV; v++) {
                 if (getenv("GB_VAR") && atoi(getenv("GB_VAR")) != v) continue;
                 a.n_tt = (n + vars[v].bt - 1) / vars[v].bt;
-                a.ks = xalm::mm_pick_ks(sh.rows, sh.K, n, (size_t)2 * 2048 * 28672, 256, vars[v].bt);
+                a.ks = xalm::mm_pick_ks(sh.rows, sh.K, n, (size_t)2 * 2048 * 28672, 256, vars[v].bt) * vars[v].kmul;
+                if (sh.K % (a.ks * 64) || (size_t)a.ks * n * sh.rows > (size_t)8 * 2048 * 28672) continue;
                 grid = a.n_rt * a.n_tt * a.ks;
                 auto launch = [&]() {
                     hipLaunchKernelGGL(vars[v].fn, dim3(grid), dim3(vars[v].threads), vars[v].lds, 0, a);

@@ -322,4 +322,10 @@ __device__ __forceinline__ u32x4 ld_sc1_x4(const void* base, const uint32_t byte
     return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)byte_off, 0, 16));
 }
 
+// silu / gelu exactly as src/infer.cpp:299-301
+__device__ __forceinline__ float act_fn(const int act, const float x) {
+    if (act == XH_ACT_SILU) return x / (1.0f + expf(-x));
+    return 0.5f * x * (1.0f + tanhf(0.797885f * (x + 0.044715f * x * x * x)));
+}
+
 }  // namespace xalm

@@ -89,11 +89,6 @@ __device__ __forceinline__ void st_sc1_f(float* p, const float v) { st_sc1_u32(p
 
 __device__ __forceinline__ float clipf(const float x, const float v) { return x < -v ? -v : (x > v ? v : x); }
 
-// silu / gelu exactly as src/infer.cpp:299-301
-__device__ __forceinline__ float act_fn(const int act, const float x) {
-    if (act == XH_ACT_SILU) return x / (1.0f + expf(-x));
-    return 0.5f * x * (1.0f + tanhf(0.797885f * (x + 0.044715f * x * x * x)));
-}
 
 // One rope rotation of the adjacent pair (v0, v1) at frequency freq (src/infer.cpp:308-321).
 __device__ __forceinline__ void rope_pair_f(float& v0, float& v1, const float freq, const int pos) {
