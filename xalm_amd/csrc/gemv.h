@@ -66,6 +66,8 @@ struct GemvArgs {
     int kv_dim;
     int head_dim;
     const float* rope_freq;  // [head_dim/2]: 1/powf(theta, j/rotary_dim) or 0 (host libm)
+    const float* rope_cs;    // [head_dim]: cosf, then sinf of (float)pos * rope_freq[j] at this step's
+                             // pos (rope_table, computed once per step by its embed kernel)
     const float* sink_cos;   // [head_dim/2]: cosf(freq) (rope at pos=1, host libm)
     const float* sink_sin;
     float qkv_clip;
@@ -110,6 +112,28 @@ __device__ __forceinline__ void rope_pair(float& v0, float& v1, const int i, con
     const float a = v0, b = v1;
     v0 = a * fcr - b * fci;
     v1 = a * fci + b * fcr;
+}
+
+// ... with the rotation's cosf / sinf given (the values rope_pair_f computes: rope_table below)
+__device__ __forceinline__ void rope_pair_cs(float& v0, float& v1, const float fcr, const float fci) {
+    const float a = v0, b = v1;
+    v0 = a * fcr - b * fci;
+    v1 = a * fci + b * fcr;
+}
+// ... at element index i from the step's table [cos | sin]
+__device__ __forceinline__ void rope_pair_tab(float& v0, float& v1, const int i, const int head_dim, const float* cs) {
+    const int j = (i % head_dim) >> 1;
+    rope_pair_cs(v0, v1, cs[j], cs[(head_dim >> 1) + j]);
+}
+// the step's rotations, by threads j < head_dim / 2 of one workgroup: cs[j] = cosf(pos * freq[j]),
+// cs[head_dim / 2 + j] = sinf(...) (rope_pair's arithmetic, src/infer.cpp:308-321, once per step
+// instead of once per row pair in every qkv epilogue)
+__device__ __forceinline__ void rope_table(float* cs, const float* freq, const int half, const int pos, const int j) {
+    if (j < half) {
+        const float val = (float)pos * freq[j];
+        cs[j] = cosf(val);
+        cs[half + j] = sinf(val);
+    }
 }
 
 // Sum of squares of x[0..n) -> rms scale 1/sqrtf(ss/n + eps), identical in every block of one
@@ -215,7 +239,7 @@ __device__ __forceinline__ void epi_st(float* p, const float v) {
 template <int ROWS>
 struct QkvPre {
     int pos, kv_pos;
-    float freq[ROWS / 2 > 0 ? ROWS / 2 : 1];
+    float cs[ROWS >= 2 ? ROWS : 2];  // (cos, sin) of each row pair's rotation
 };
 // res: EPI_RESID's residual rows, requested with the group's first weights (not from the
 // epilogue, where the load would be a dependent round trip at the group's end)
@@ -254,16 +278,16 @@ __device__ __forceinline__ void gemv_epilogue(const GemvArgs& a, const int row0,
             const int row = row0 + p;
             float v0 = clipf(acc[p], a.qkv_clip), v1 = clipf(acc[p + 1], a.qkv_clip);
             if (row < a.q_dim) {
-                if (pre) rope_pair_f(v0, v1, pre->freq[p >> 1], pos);
-                else rope_pair(v0, v1, row, a.head_dim, pos, a.rope_freq);
+                if (pre) rope_pair_cs(v0, v1, pre->cs[p], pre->cs[p + 1]);
+                else rope_pair_tab(v0, v1, row, a.head_dim, a.rope_cs);
                 epi_st<SC1>(a.q + row, v0);
                 epi_st<SC1>(a.q + row + 1, v1);
             } else {
                 const bool isk = row < a.q_dim + a.kv_dim;
                 const int kr = isk ? row - a.q_dim : row - a.q_dim - a.kv_dim;
                 if (isk) {
-                    if (pre) rope_pair_f(v0, v1, pre->freq[p >> 1], pos);  // q_dim % head_dim == 0
-                    else rope_pair(v0, v1, kr, a.head_dim, pos, a.rope_freq);
+                    if (pre) rope_pair_cs(v0, v1, pre->cs[p], pre->cs[p + 1]);  // q_dim % head_dim == 0
+                    else rope_pair_tab(v0, v1, kr, a.head_dim, a.rope_cs);
                 }
                 uint16_t* dst = (isk ? a.kcache : a.vcache) + (size_t)kv_pos * a.kv_dim + kr;
                 // the pair as one 4-byte store (kr is even)
@@ -615,13 +639,17 @@ __device__ __forceinline__ void gemv_rows_pipe(const GemvArgs& a, const int g0, 
     // QKV: requested with the weights, ahead of the epilogue that uses them.  One-byte weights
     // only: fp8 decode 596 -> 603 tok/s, while the 2-byte qkv launch measured 0.5 % slower with it
     // (same-box A/B, two pairs each)
+#ifdef QKV_PRE_ALL
+    constexpr bool QKV = EPI == EPI_QKV;
+#else
     constexpr bool QKV = EPI == EPI_QKV && E >= 16;
+#endif
     QkvPre<ROWS> qp{};
     if constexpr (QKV) {
         qp.pos = a.sp->pos;
         qp.kv_pos = a.sp->kv_pos;
     }
-    // QKV: the rope frequency of each row pair of the step's group; RESID: its residual rows
+    // QKV: the rotation (cos, sin) of each row pair of the step's group; RESID: its residual rows
     constexpr bool RES = EPI == EPI_RESID && !SC1;
     float fa[ROWS], fb[ROWS];
     auto load = [&](u32x4 (&w)[U][ROWS], float (&d)[U][ROWS], float (&f)[ROWS], const int k) {
@@ -633,7 +661,11 @@ __device__ __forceinline__ void gemv_rows_pipe(const GemvArgs& a, const int g0, 
         if constexpr (QKV) {
             const int row0 = min((g0 + q * total_waves) * ROWS, a.rows - ROWS);
 #pragma unroll
-            for (int p = 0; p < ROWS; p += 2) f[p >> 1] = a.rope_freq[((row0 + p) % a.head_dim) >> 1];
+            for (int p = 0; p < ROWS; p += 2) {
+                const int j = ((row0 + p) % a.head_dim) >> 1;
+                f[p] = a.rope_cs[j];
+                f[p + 1] = a.rope_cs[(a.head_dim >> 1) + j];
+            }
         }
         if constexpr (RES) {
             const int row0 = (g0 + q * total_waves) * ROWS;
@@ -655,7 +687,7 @@ __device__ __forceinline__ void gemv_rows_pipe(const GemvArgs& a, const int g0, 
             for (int r = 0; r < ROWS; r++) acc[r] = wave_sum(acc[r]);
             if constexpr (QKV) {
 #pragma unroll
-                for (int p = 0; p < ROWS; p += 2) qp.freq[p >> 1] = f[p >> 1];
+                for (int p = 0; p < ROWS; p++) qp.cs[p] = f[p];
             }
             if (lane == 0)
                 gemv_epilogue<EPI, ROWS, SC1>(a, (g0 + q * total_waves) * ROWS, acc, best, QKV ? &qp : nullptr,
@@ -677,7 +709,11 @@ __device__ __forceinline__ void gemv_rows_pipe(const GemvArgs& a, const int g0, 
         if constexpr (QKV) {
             const int row0 = min(g0 * ROWS, a.rows - ROWS);
 #pragma unroll
-            for (int p = 0; p < ROWS; p += 2) fa[p >> 1] = a.rope_freq[((row0 + p) % a.head_dim) >> 1];
+            for (int p = 0; p < ROWS; p += 2) {
+                const int j = ((row0 + p) % a.head_dim) >> 1;
+                fa[p] = a.rope_cs[j];
+                fa[p + 1] = a.rope_cs[(a.head_dim >> 1) + j];
+            }
         }
         if constexpr (RES) {
 #pragma unroll

@@ -31,9 +31,11 @@ __global__ void rope_kernel(float* vec, int d, int head_dim, int pos, const floa
 }
 
 // Model::_copy_embedding (src/infer.cpp:553-602): x = dec(embed[token, :])
-__global__ void embed_kernel(const void* emb, int dtype, int dim, float* x, const StepParams* sp) {
+__global__ void embed_kernel(const void* emb, int dtype, int dim, float* x, const StepParams* sp,
+                             const float* rope_freq, float* rope_cs, int half) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < dim) x[i] = dec_row(dtype, emb, (size_t)sp->token, dim, i);
+    if (blockIdx.x == 0) rope_table(rope_cs, rope_freq, half, sp->pos, threadIdx.x);
 }
 
 // Greedy decode step head: argmax over the lm_head workgroups' candidates (Sampler::
@@ -44,9 +46,10 @@ __global__ void embed_kernel(const void* emb, int dtype, int dim, float* x, cons
 constexpr int ARGMAX_CANDS = 1024;
 __global__ __launch_bounds__(1024) void argmax_embed_kernel(const unsigned long long* cand, StepParams* sp,
                                                             int* tokens, int cap, const void* emb, int dtype,
-                                                            int dim, float* x) {
+                                                            int dim, float* x, const float* rope_freq,
+                                                            float* rope_cs, int half) {
     __shared__ unsigned long long kb[16];
-    __shared__ int tok_s;
+    __shared__ int tok_s, pos_s;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     unsigned long long best = cand[tid];  // ARGMAX_CANDS == blockDim.x
 #pragma unroll
@@ -67,8 +70,10 @@ __global__ __launch_bounds__(1024) void argmax_embed_kernel(const unsigned long 
         step_positions(sp, sp->pos_next);
         sp->pos_next += 1;
         tok_s = tok;
+        pos_s = sp->pos;
     }
     __syncthreads();
+    rope_table(rope_cs, rope_freq, half, pos_s, tid);
     for (int i = tid; i < dim; i += 1024) x[i] = dec_row(dtype, emb, (size_t)tok_s, dim, i);
 }
 

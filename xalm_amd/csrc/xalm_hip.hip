@@ -113,6 +113,7 @@ struct xh_ctx {
     float *part_o = nullptr, *part_ml = nullptr;
     int* attn_cnt = nullptr;        // [n_kv_heads] split arrival tickets
     float *rope_freq = nullptr, *sink_cos = nullptr, *sink_sin = nullptr;
+    float* rope_cs = nullptr;  // [head_dim]: this step's rotations (rope_table, gemv.h)
     StepParams* sp = nullptr;       // device
     StepParams* sp_host = nullptr;  // pinned
     int* dec_tokens = nullptr;      // device, decode loop output
@@ -406,7 +407,7 @@ GemvArgs qkv_args(xh_ctx* ctx, int l) {
     a.norm_w = w.attn_norm; a.norm_dtype = w.an_dt; a.eps = ctx->c.norm_eps;
     a.q = ctx->q; a.kcache = ctx->kcache(l); a.vcache = ctx->vcache(l);
     a.q_dim = ctx->q_dim; a.kv_dim = ctx->kv_dim; a.head_dim = ctx->c.head_dim;
-    a.rope_freq = ctx->rope_freq; a.sink_cos = ctx->sink_cos; a.sink_sin = ctx->sink_sin;
+    a.rope_freq = ctx->rope_freq; a.rope_cs = ctx->rope_cs; a.sink_cos = ctx->sink_cos; a.sink_sin = ctx->sink_sin;
     a.qkv_clip = ctx->c.qkv_clip; a.sp = ctx->sp;
     if (layer_traced(ctx, l)) a.trace = ctx->aw_trace + LT_QKV;
     return a;
@@ -537,10 +538,11 @@ int enqueue_step(xh_ctx* ctx, hipStream_t s, bool with_logits, bool greedy = fal
     if (greedy)
         hipLaunchKernelGGL(argmax_embed_kernel, dim3(1), dim3(ARGMAX_CANDS), 0, s, (const unsigned long long*)ctx->cand,
                            ctx->sp, ctx->dec_tokens, ctx->dec_cap, (const void*)ctx->embed, ctx->embed_dt, c.dim,
-                           ctx->x);
+                           ctx->x, (const float*)ctx->rope_freq, ctx->rope_cs, c.head_dim / 2);
     else
         hipLaunchKernelGGL(embed_kernel, dim3((c.dim + 255) / 256), dim3(256), 0, s, (const void*)ctx->embed,
-                           ctx->embed_dt, c.dim, ctx->x, (const StepParams*)ctx->sp);
+                           ctx->embed_dt, c.dim, ctx->x, (const StepParams*)ctx->sp, (const float*)ctx->rope_freq,
+                           ctx->rope_cs, c.head_dim / 2);
     for (int l = 0; l < c.n_layers; l++) {
         const LayerW& w = ctx->L[l];
         if (!launch_gemv<PRO_RMSNORM, EPI_QKV>(kdt(w.qkv_dt, w.qkv_x), qkv_args(ctx, l), s, qkv_launch_waves(ctx, l)))
@@ -1406,6 +1408,7 @@ int xh_create(const xh_config* cfg, int device_ordinal, xh_ctx** out) {
     ctx->aw_trace_len = (size_t)8 * ((size_t)c.n_kv_heads * ctx->nsplit + 4096);
     CREATE_TRY(dmalloc(ctx, &ctx->aw_trace, ctx->aw_trace_len));
     CREATE_TRY(dmalloc(ctx, &ctx->rope_freq, (size_t)c.head_dim / 2));
+    CREATE_TRY(dmalloc(ctx, &ctx->rope_cs, (size_t)c.head_dim));
     CREATE_TRY(dmalloc(ctx, &ctx->sink_cos, (size_t)c.head_dim / 2));
     CREATE_TRY(dmalloc(ctx, &ctx->sink_sin, (size_t)c.head_dim / 2));
     CREATE_TRY(dmalloc(ctx, &ctx->sp, 1));
@@ -1453,7 +1456,7 @@ void xh_destroy(xh_ctx* ctx) {
     hipFree(ctx->kv); hipFree(ctx->x); hipFree(ctx->q); hipFree(ctx->attn_out); hipFree(ctx->hb);
     hipFree(ctx->logits); hipFree(ctx->part_o); hipFree(ctx->part_ml); hipFree(ctx->attn_cnt); hipFree(ctx->aw_sync); hipFree(ctx->cand); hipFree(ctx->scan_flag);
     pf_free(ctx);
-    hipFree(ctx->pf_wdq); hipFree(ctx->ppl_tgt); hipFree(ctx->ppl_prob); hipFree(ctx->rope_freq);
+    hipFree(ctx->pf_wdq); hipFree(ctx->ppl_tgt); hipFree(ctx->ppl_prob); hipFree(ctx->rope_freq); hipFree(ctx->rope_cs);
     hipFree(ctx->aw_trace);
     for (auto& kv : ctx->blas_plans) {
         const xh_ctx::BlasPlan& p = kv.second;
