@@ -638,12 +638,8 @@ __device__ __forceinline__ void gemv_rows_pipe(const GemvArgs& a, const int g0, 
     const int total = ((n_groups - g0 + total_waves - 1) / total_waves) * steps;
     // QKV: requested with the weights, ahead of the epilogue that uses them.  One-byte weights
     // only: fp8 decode 596 -> 603 tok/s, while the 2-byte qkv launch measured 0.5 % slower with it
-    // (same-box A/B, two pairs each)
-#ifdef QKV_PRE_ALL
-    constexpr bool QKV = EPI == EPI_QKV;
-#else
+    // (same-box A/B, two pairs each; again with the rope table: 393.3 vs 391.2 tok/s, 3 pairs)
     constexpr bool QKV = EPI == EPI_QKV && E >= 16;
-#endif
     QkvPre<ROWS> qp{};
     if constexpr (QKV) {
         qp.pos = a.sp->pos;
