@@ -193,9 +193,10 @@ int xh_set_graphs(xh_ctx* ctx, int enable);
  * build); 0 = one forward per token (the reference's loop, src/main.cpp:94-100).  Same math per
  * token up to f32 rounding. */
 /* XH_OPT_PREFILL_GLU_SPLIT (default 1): where the W2 GEMM takes split-f16 input, the GLU
- * epilogue of the W1/W3 GEMM writes those f16 hi/lo halves directly (one launch); 0 = GLU to
- * f32 first, then split in the W2 GEMM's input pass (two launches).  Bit-identical results; a
- * debug knob so tests cover both routes. */
+ * epilogue of the W1/W3 GEMM writes those f16 hi/lo halves directly (one launch), and each
+ * residual add runs in one launch with the following rmsnorm split; 0 = GLU to f32 first, then
+ * split in the W2 GEMM's input pass, and residual and rmsnorm as separate launches.
+ * Bit-identical results; a debug knob so tests cover both routes. */
 /* XH_OPT_PREFILL_ATTN (default 1): the batched path's causal attention on MFMA tiles (32 query
  * rows x 32-slot K/V tiles per wave, running max/sum, q and p as exact f16 hi + lo pairs), the
  * K/V tiles shared by the 4 waves of a workgroup through an LDS ring (head_dim 128); 2 = the same

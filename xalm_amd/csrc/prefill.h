@@ -301,6 +301,103 @@ __global__ __launch_bounds__(256) void prefill_rmsnorm_split_kernel(const float*
     if (threadIdx.x == 0) inv_s[t] = 1.f / s;
 }
 
+// EPI_RESID of a GEMM's partials (x += the summed K-slices, slice order, times part_s, as
+// prefill_epi_kernel) and the rmsnorm split of the updated row for the next GEMM (as
+// prefill_rmsnorm_split_kernel: the same per-thread float4 order, reduction and split), in one
+// launch: the residual row is read once.  part_s and inv_s may both be pf_xs: a workgroup reads
+// its token's factor before the first barrier and writes the new one after the last.  Dynamic
+// LDS: the updated row (dim floats).  grid = 32 x token tiles; rows past n are zero.
+__global__ __launch_bounds__(256) void prefill_resid_norm_split_kernel(const float* part, int ks, const float* part_s,
+                                                                       float* x, int dim, const void* w, int wdt,
+                                                                       float eps, int n, int E, uint16_t* xh,
+                                                                       uint16_t* xl, float* inv_s) {
+    extern __shared__ float xrow[];
+    __shared__ float red[4];
+    const int t = blockIdx.x;
+    auto frag = [&](const int k) { return split_off(t, k, dim, E); };
+    if (t >= n) {
+        for (int i = threadIdx.x; i < dim / 8; i += 256) {
+            const size_t o = frag(8 * i);
+            *(u32x4*)(xh + o) = u32x4{0u, 0u, 0u, 0u};
+            *(u32x4*)(xl + o) = u32x4{0u, 0u, 0u, 0u};
+        }
+        return;
+    }
+    float4* xr4 = (float4*)(x + (size_t)t * dim);
+    const float ps = part_s ? part_s[t] : 1.f;
+    float ss = 0.f;
+    for (int i = threadIdx.x; i < (dim >> 2); i += 256) {
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int s = 0; s < ks; s++) {  // slice order: fixed
+            const float4 p = *(const float4*)(part + ((size_t)s * n + t) * dim + 4 * i);
+            v.x += p.x;
+            v.y += p.y;
+            v.z += p.z;
+            v.w += p.w;
+        }
+        if (part_s) {
+            v.x *= ps;
+            v.y *= ps;
+            v.z *= ps;
+            v.w *= ps;
+        }
+        float4 r = xr4[i];
+        r.x += v.x;
+        r.y += v.y;
+        r.z += v.z;
+        r.w += v.w;
+        xr4[i] = r;
+        ((float4*)xrow)[i] = r;
+        ss += r.x * r.x + r.y * r.y + r.z * r.z + r.w * r.w;
+    }
+    // block_rms_scale<256>'s reduction
+    ss = wave_sum(ss);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
+    __syncthreads();
+    float tot = 0.f;
+#pragma unroll
+    for (int wv = 0; wv < 4; wv++) tot += red[wv];
+    const float rms = sqrtf(tot / (float)dim + eps);
+    const float scale = 1.0f / rms;
+    __syncthreads();  // red reused below
+    auto norm8 = [&](const int i, float* v) {  // elements 8i .. 8i+7 of the normed row
+        const float4 a = ((const float4*)xrow)[2 * i], b = ((const float4*)xrow)[2 * i + 1];
+        const float4 wa = load_norm4(w, wdt, 2 * i), wb = load_norm4(w, wdt, 2 * i + 1);
+        v[0] = a.x * scale * wa.x; v[1] = a.y * scale * wa.y; v[2] = a.z * scale * wa.z; v[3] = a.w * scale * wa.w;
+        v[4] = b.x * scale * wb.x; v[5] = b.y * scale * wb.y; v[6] = b.z * scale * wb.z; v[7] = b.w * scale * wb.w;
+    };
+    float m = 0.f;
+    for (int i = threadIdx.x; i < dim / 8; i += 256) {
+        float v[8];
+        norm8(i, v);
+#pragma unroll
+        for (int j = 0; j < 8; j++) m = fmaxf(m, fabsf(v[j]));
+    }
+    m = wave_max(m);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+    __syncthreads();
+    m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    int e = 0;
+    const bool ok = m > 0.f && m <= FLT_MAX;
+    if (ok) frexpf(m, &e);
+    const float s = ok ? ldexpf(1.f, 15 - e) : 1.f;
+    for (int i = threadIdx.x; i < dim / 8; i += 256) {
+        float v[8];
+        norm8(i, v);
+        f16x8 hi, lo;
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const float u = v[j] * s;
+            hi[j] = (_Float16)u;
+            lo[j] = (_Float16)(u - (float)hi[j]);
+        }
+        const size_t o = frag(8 * i);
+        *(f16x8*)(xh + o) = hi;
+        *(f16x8*)(xl + o) = lo;
+    }
+    if (threadIdx.x == 0) inv_s[t] = 1.f / s;
+}
+
 // EPI_GLU (act(g) * u of the summed K-slices, slice order as prefill_epi_kernel) written
 // straight into the split-f16 fragments of the W2 GEMM's input: one launch instead of GLU
 // epilogue + split.  The row (hidden f32) is held in dynamic LDS between the max and the split

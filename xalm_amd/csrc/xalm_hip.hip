@@ -148,6 +148,7 @@ struct xh_ctx {
     uint16_t* pf_wdq = nullptr;                  // f16 image of one fp8 matrix for the f16 GEMMs (pf_prepare)
     size_t pf_wdq_elems = 0;
     bool pf_split_ready = false;                 // pf_norm left the next GEMM's split input
+    bool pf_resid_norm = true;                   // residual + rmsnorm split in one launch (XH_OPT_PREFILL_GLU_SPLIT 0: off)
     bool pf_glu_split = true;                    // XH_OPT_PREFILL_GLU_SPLIT: fused GLU -> split input
     int pf_attn_mode = 1;                        // XH_OPT_PREFILL_ATTN: 1 shared-tile MFMA (v1 for head_dim != 128),
                                                  // 2 per-wave MFMA tiles, 0 per-token split kernel
@@ -1097,6 +1098,27 @@ int pf_gemm(xh_ctx* ctx, const char* what, int dt, const void* w, int K, int row
     ks = a.ks;
     return 0;
 }
+void pf_epi(xh_ctx* ctx, PfEpiArgs e);
+// x += the last GEMM's partials (EPI_RESID), then the rmsnorm of the updated rows as the input of
+// the GEMM over W (dt, [rows][dim]): one launch when that GEMM takes the split input and the
+// rows fit the LDS, else pf_epi + pf_norm (the same bits either way)
+void pf_resid_norm(xh_ctx* ctx, int ks, const void* nw, int ndt, int m, int dt, int rows) {
+    const xh_config& c = ctx->c;
+    const int lay = pf_layout(ctx, dt, c.dim, rows);
+    const size_t lds = (size_t)c.dim * sizeof(float);
+    if (lay >= 0 && ctx->pf_resid_norm && c.dim % 8 == 0 && lds <= 64 * 1024) {
+        hipLaunchKernelGGL(prefill_resid_norm_split_kernel, dim3(pf_split_grid(lay, m)), dim3(256), lds, ctx->stream,
+                           (const float*)ctx->pf_part, ks, (const float*)(ctx->pf_scaled ? ctx->pf_xs : nullptr),
+                           ctx->pf_x, c.dim, nw, ndt, c.norm_eps, m, lay, ctx->pf_xh, pf_lo(ctx, lay, m, c.dim),
+                           ctx->pf_xs);
+        ctx->pf_split_ready = true;
+        return;
+    }
+    PfEpiArgs e{};
+    e.ks = ks; e.n = m; e.rows = c.dim; e.epi = EPI_RESID; e.out = ctx->pf_x;
+    pf_epi(ctx, e);
+    pf_norm(ctx, nw, ndt, m, dt, rows);
+}
 void pf_epi(xh_ctx* ctx, PfEpiArgs e) {
     e.part = ctx->pf_part;
     e.part_s = ctx->pf_scaled ? ctx->pf_xs : nullptr;
@@ -1223,7 +1245,8 @@ int prefill_batched(xh_ctx* ctx, const int* tokens, int n, int pos0, int want_lo
             // attention block (src/infer.cpp:380-452)
             const int qkv_rows = ctx->q_dim + 2 * ctx->kv_dim;
             int ks = 0;
-            pf_norm(ctx, w.attn_norm, w.an_dt, m, kdt(w.qkv_dt, w.qkv_x), qkv_rows);
+            // layers after the first: the previous W2 residual and this rmsnorm ran as one launch
+            if (l == 0) pf_norm(ctx, w.attn_norm, w.an_dt, m, kdt(w.qkv_dt, w.qkv_x), qkv_rows);
             if ((rc = pf_gemm(ctx, "qkv", kdt(w.qkv_dt, w.qkv_x), w.wqkv, c.dim, qkv_rows, ctx->pf_xn, m, ks))) return rc;
             PfEpiArgs e{};
             e.ks = ks; e.n = m; e.rows = qkv_rows; e.epi = EPI_QKV; e.q = ctx->pf_q;
@@ -1236,11 +1259,8 @@ int prefill_batched(xh_ctx* ctx, const int* tokens, int n, int pos0, int want_lo
             aa.nsplit = std::min(ctx->nsplit, std::max(1, (p0 + m + ATTN_MIN_T - 1) / ATTN_MIN_T));
             if ((rc = pf_attn(ctx, aa, m, p0))) return rc;
             if ((rc = pf_gemm(ctx, "wo", kdt(w.wo_dt, w.wo_x), w.wo, ctx->q_dim, c.dim, ctx->pf_att, m, ks))) return rc;
-            e = PfEpiArgs{};
-            e.ks = ks; e.n = m; e.rows = c.dim; e.epi = EPI_RESID; e.out = ctx->pf_x;
-            pf_epi(ctx, e);
-            // feed-forward block (src/infer.cpp:455-494)
-            pf_norm(ctx, w.ffn_norm, w.fn_dt, m, kdt(w.w13_dt, w.w13_x), 2 * c.hidden_dim);
+            // residual, then the feed-forward block's rmsnorm (src/infer.cpp:449-452, 455-494)
+            pf_resid_norm(ctx, ks, w.ffn_norm, w.fn_dt, m, kdt(w.w13_dt, w.w13_x), 2 * c.hidden_dim);
             if ((rc = pf_gemm(ctx, "w1/w3", kdt(w.w13_dt, w.w13_x), w.w13, c.dim, 2 * c.hidden_dim, ctx->pf_xn, m, ks)))
                 return rc;
             const int lay2 = pf_layout(ctx, kdt(w.w2_dt, w.w2_x), c.hidden_dim, c.dim);
@@ -1267,9 +1287,15 @@ int prefill_batched(xh_ctx* ctx, const int* tokens, int n, int pos0, int want_lo
                 pf_epi(ctx, e);
             }
             if ((rc = pf_gemm(ctx, "w2", kdt(w.w2_dt, w.w2_x), w.w2, c.hidden_dim, c.dim, ctx->pf_h, m, ks))) return rc;
-            e = PfEpiArgs{};
-            e.ks = ks; e.n = m; e.rows = c.dim; e.epi = EPI_RESID; e.out = ctx->pf_x;
-            pf_epi(ctx, e);
+            if (l + 1 < c.n_layers) {
+                // residual, then the next layer's attention rmsnorm (src/infer.cpp:491-494, 380)
+                const LayerW& wn = ctx->L[l + 1];
+                pf_resid_norm(ctx, ks, wn.attn_norm, wn.an_dt, m, kdt(wn.qkv_dt, wn.qkv_x), qkv_rows);
+            } else {
+                e = PfEpiArgs{};
+                e.ks = ks; e.n = m; e.rows = c.dim; e.epi = EPI_RESID; e.out = ctx->pf_x;
+                pf_epi(ctx, e);
+            }
         }
         if (probs) {
             // Model::forward's OUTPUT_LOGITS tail (src/infer.cpp:620-637) for every token of the
@@ -2021,6 +2047,7 @@ int xh_set_option(xh_ctx* ctx, int option, int value) {
         case XH_OPT_PREFILL_GLU_SPLIT:
             if (value < 0 || value > 1) return set_err(ctx, XH_E_INVALID, "XH_OPT_PREFILL_GLU_SPLIT: 0 or 1");
             ctx->pf_glu_split = value != 0;
+            ctx->pf_resid_norm = value != 0;
             return 0;
         case XH_OPT_PREFILL_ATTN:
             if (value < 0 || value > 2) return set_err(ctx, XH_E_INVALID, "XH_OPT_PREFILL_ATTN: 0, 1 or 2");
