@@ -355,6 +355,10 @@ def main():
                     help="also time xh_prefill of this many prompt tokens (batched path; 0 = skip)")
     ap.add_argument("--fuse-attn-wo", type=int, default=1, choices=(0, 1),
                     help="attention + Wo in one launch (1) or two launches (0)")
+    ap.add_argument("--pos0", type=int, default=0,
+                    help="4k workloads: ring slots [0, pos0) hold a synthetic K/V history and the prompt is "
+                         "hydrated at pos0 (e.g. 3808: the timed tokens end at kv_len 4096, the worst token of "
+                         "the 4k context, SURVEY 8d)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -388,9 +392,18 @@ def main():
             model.kv_fill_synthetic(layer, 0, 0, w["kv_prefill"], 5000 + 2 * layer, 1.0)
             model.kv_fill_synthetic(layer, 1, 0, w["kv_prefill"], 5001 + 2 * layer, 1.0)
         pos0 = w["kv_prefill"]
+    elif args.pos0:
+        if args.pos0 + len(prompt) + args.warmup + args.steps > c.max_seq_len:
+            raise SystemExit(f"--pos0 {args.pos0}: prompt + warmup + steps exceed the {c.max_seq_len} context")
+        for layer in range(c.n_layers):
+            model.kv_fill_synthetic(layer, 0, 0, args.pos0, 5000 + 2 * layer, 1.0)
+            model.kv_fill_synthetic(layer, 1, 0, args.pos0, 5001 + 2 * layer, 1.0)
+        pos0 = args.pos0
     model.prefill(prompt[:1] if w["kv_prefill"] else prompt, pos0, st)
     pos = pos0 + (1 if w["kv_prefill"] else len(prompt))
     logits0 = st.logits().copy()
+    if args.pos0 and not w["kv_prefill"]:
+        args.no_cpu_baseline = True  # the CPU baseline's oracle starts from an empty ring
 
     warm_tokens = model.decode_greedy(pos, args.warmup) if args.warmup else []
     pos += args.warmup
@@ -480,8 +493,25 @@ def main():
             sync_all(None, torch_mod)
             res[name] = round(args.prefill_tokens / (time.perf_counter() - t0), 1)
         model.set_option(L.OPT_PREFILL_ATTN, 1)
+        # short passes at the end of the ring (resuming a long chat): the prompt attention's
+        # history splits (XH_OPT_PREFILL_ATTN_SPLIT 1) against one walk per workgroup (0)
+        short = {}
+        for n in (1, 32, 256):
+            stoks = prompt_tokens(c.vocab_size, n=n, seed=17)
+            p0s = c.max_seq_len - n
+            for split in (1, 0):
+                model.set_option(L.OPT_PREFILL_ATTN_SPLIT, split)
+                model.prefill(stoks, p0s, st)  # warm
+                sync_all(None, torch_mod)
+                t0 = time.perf_counter()
+                model.prefill(stoks, p0s, st)
+                sync_all(None, torch_mod)
+                short[f"{n}_tok_split{split}_ms"] = round(1e3 * (time.perf_counter() - t0), 3)
+        model.set_option(L.OPT_PREFILL_ATTN_SPLIT, 1)
         prefill = {"tokens": args.prefill_tokens, "pos0": p0, "tok_s_by_attention": res,
-                   "note": "prompt pass at the end of the -T 32768 ring: each token attends over ~30k slots"}
+                   "short_passes_at_ring_end": short,
+                   "note": "prompt pass at the end of the -T 32768 ring: each token attends over ~30k slots; "
+                           "short_passes: wall ms of one xh_prefill of n tokens at pos0 = 32768 - n"}
 
     cpu = None
     if cpu_n:
@@ -514,6 +544,7 @@ def main():
             "dtype": w["dtype"],
             "data": "synthetic (deterministic xalm_synth weights of the named shapes; no checkpoint offline)",
             "config": {"workload": w["desc"], "prompt_tokens": len(prompt), "max_seq_len": c.max_seq_len,
+                       "history_pos0": pos0,
                        "kv_len_timed": [pos + 1, pos + args.steps], "batch": 1, "parallelism": f"replicas x{world}",
                        "engine": {1: "hipGraph per token, attention+Wo fused",
                                   0: "hipGraph per token"}[model.get_option(L.OPT_FUSE_ATTN_WO)]},

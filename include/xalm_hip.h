@@ -204,7 +204,17 @@ int xh_set_graphs(xh_ctx* ctx, int enable);
  * token and KV head, split-KV (the decode attention's blocks).
  * Option id 4 (XH_OPT_COL_KV_MAX, removed in round 3 with the column-form attention) is no
  * longer accepted: xh_set_option / xh_get_option return XH_E_INVALID for it. */
-enum xh_option { XH_OPT_FUSE_ATTN_WO = 1, XH_OPT_PREFILL = 2, XH_OPT_PREFILL_GLU_SPLIT = 3, XH_OPT_PREFILL_ATTN = 5 };
+/* XH_OPT_PREFILL_ATTN_SPLIT (default 1): under XH_OPT_PREFILL_ATTN 1, a pass too short to fill the
+ * chip with (KV head, 128-row query tile) workgroups walks a long history in splits (each with its
+ * own running max / sum), merged per row in split order afterwards (deterministic); 0 = one
+ * workgroup walks the whole history.  Same math up to f32 rounding. */
+enum xh_option {
+    XH_OPT_FUSE_ATTN_WO = 1,
+    XH_OPT_PREFILL = 2,
+    XH_OPT_PREFILL_GLU_SPLIT = 3,
+    XH_OPT_PREFILL_ATTN = 5,
+    XH_OPT_PREFILL_ATTN_SPLIT = 6
+};
 int xh_set_option(xh_ctx* ctx, int option, int value);
 int xh_get_option(const xh_ctx* ctx, int option, int* value);
 

@@ -394,6 +394,7 @@ def test_prompt_attention_shared_tiles_bit_identical(heads, kv_heads):
         gm, om = build_pair(c, L.F16)
         om.close()
         gm.set_option(L.OPT_PREFILL_ATTN, attn)
+        gm.set_option(L.OPT_PREFILL_ATTN_SPLIT, 0)  # one walk of the history per workgroup, as mode 2
         st = InferenceState(c)
         for a, b in zip(cuts[:-1], cuts[1:]):
             gm.prefill(toks[a:b], a, st)
@@ -405,8 +406,8 @@ def test_prompt_attention_shared_tiles_bit_identical(heads, kv_heads):
         assert np.array_equal(a, b)
 
 
-@pytest.mark.parametrize("attn", [1, 2, 0])
-def test_prompt_over_long_history(attn):
+@pytest.mark.parametrize("attn,split", [(1, 1), (1, 0), (2, 0), (0, 0)])
+def test_prompt_over_long_history(attn, split):
     """A 200-token prompt pass at pos0 = 12000 over a synthetic 12000-slot KV history (8 KV heads x
     head_dim 128, 4 q per KV head): every token's attention walks ~375 K/V tiles through the
     shared-tile ring (1), the per-wave tiles (2) or the split-KV kernel (0).  Last logits and the
@@ -414,6 +415,7 @@ def test_prompt_over_long_history(attn):
     c = make_cfg(256, 512, 2, 32, 8, 128, 512, 16384)
     gm, om = build_pair(c, L.F16)
     gm.set_option(L.OPT_PREFILL_ATTN, attn)
+    gm.set_option(L.OPT_PREFILL_ATTN_SPLIT, split)  # 1: 56 workgroups -> 10 history splits each
     history, n = 12000, 200
     kv_dim = c.n_kv_heads * c.head_dim
     for layer in range(c.n_layers):
@@ -433,5 +435,45 @@ def test_prompt_over_long_history(attn):
             a = f16(gm.kv_read(layer, which, history, n))
             b = f16(om.kv(layer, which)[history:history + n])
             assert np.abs(a - b).max() <= 2e-3 * max(1.0, np.abs(b).max()), (layer, which)
+    gm.close()
+    om.close()
+
+
+@pytest.mark.parametrize("n", [1, 32, 256])
+def test_short_prompt_over_32k_history(n):
+    """Short prompt passes over a ~32.7k-slot history at configs[3]'s head shape (32 q heads, 8 KV
+    heads, head_dim 128; src/main.cpp:94-100 resuming a long chat): a pass of n tokens has
+    8 * ceil(n / 32) (KV head, query tile) workgroups, so XH_OPT_PREFILL_ATTN_SPLIT 1 walks the
+    history in up to 64 splits merged in split order.  Both the split and the single-walk forms
+    against the oracle's token loop (last logits, the pass's K/V rows), and the split form
+    repeatable bit for bit (fixed merge order)."""
+    c = make_cfg(256, 512, 2, 32, 8, 128, 512, 32768)
+    gm, om = build_pair(c, L.F16)
+    history = c.max_seq_len - 8 - n  # the pass ends inside the ring (no wrap: the batched path)
+    kv_dim = c.n_kv_heads * c.head_dim
+    for layer in range(c.n_layers):
+        for which in (0, 1):
+            seed = 3300 + 2 * layer + which
+            gm.kv_fill_synthetic(layer, which, 0, history, seed, 1.0)
+            om.set_kv(layer, which, 0, O.synthetic(history, kv_dim, L.F16, seed, 0.0, 1.0))
+    toks = [3 + (i * 31) % 500 for i in range(n)]
+    for i, tok in enumerate(toks):
+        om.forward(tok, history + i, L.OUTPUT_LOGITS if i == n - 1 else L.HYDRATE_KV_CACHE)
+    ref = om.logits()
+    st = InferenceState(c)
+    got = {}
+    for split in (1, 0, 1):
+        gm.set_option(L.OPT_PREFILL_ATTN_SPLIT, split)
+        gm.prefill(toks, history, st)
+        lg = st.logits().copy()
+        assert np.abs(lg - ref).max() <= bar(ref), (split, float(np.abs(lg - ref).max()))
+        for layer in range(c.n_layers):
+            for which in (0, 1):
+                a = f16(gm.kv_read(layer, which, history, n))
+                b = f16(om.kv(layer, which)[history:history + n])
+                assert np.abs(a - b).max() <= 2e-3 * max(1.0, np.abs(b).max()), (split, layer, which)
+        if split in got:
+            assert np.array_equal(lg.view(np.uint32), got[split].view(np.uint32))
+        got[split] = lg
     gm.close()
     om.close()

@@ -61,6 +61,7 @@ static float blaslt_us(hipblasLtHandle_t h, int rows, int K, int n2, void* W, vo
 }
 
 int main(int argc, char** argv) {
+    setvbuf(stdout, nullptr, _IOLBF, 0);  // a line reaches the log as soon as it is printed
     std::vector<int> ns;
     for (int i = 1; i < argc; i++) ns.push_back(atoi(argv[i]));
     if (ns.empty()) ns = {512, 1024, 2048};
@@ -137,7 +138,7 @@ int main(int argc, char** argv) {
                 if (getenv("GB_VAR") && atoi(getenv("GB_VAR")) != v) continue;
                 a.n_tt = (n + vars[v].bt - 1) / vars[v].bt;
                 a.ks = xalm::mm_pick_ks(sh.rows, sh.K, n, (size_t)2 * 2048 * 28672, 256, vars[v].bt) * vars[v].kmul;
-                if (sh.K % (a.ks * 64) || (size_t)a.ks * n * sh.rows > (size_t)8 * 2048 * 28672) continue;
+                if (a.ks <= 0 || sh.K % (a.ks * 64) || (size_t)a.ks * n * sh.rows > (size_t)8 * 2048 * 28672) continue;
                 grid = a.n_rt * a.n_tt * a.ks;
                 auto launch = [&]() {
                     hipLaunchKernelGGL(vars[v].fn, dim3(grid), dim3(vars[v].threads), vars[v].lds, 0, a);
@@ -188,5 +189,13 @@ int main(int argc, char** argv) {
         for (int v = 0; v < NV; v++)
             printf("    %-8s %8.1f us = %6.1f TF/s\n", vars[v].name, tot_us[v], tot_flop / tot_us[v] * 1e-6);
     }
+    CK(hipEventDestroy(e0));
+    CK(hipEventDestroy(e1));
+    CB(hipblasLtDestroy(bl));
+    CK(hipFree(ws));
+    CK(hipFree(dy));
+    CK(hipFree(dx));
+    CK(hipFree(dw));
+    printf("done: %d bad\n", bad);
     return bad ? 1 : 0;
 }

@@ -32,6 +32,7 @@ OPT_FUSE_ATTN_WO = 1
 OPT_PREFILL = 2
 OPT_PREFILL_GLU_SPLIT = 3
 OPT_PREFILL_ATTN = 5
+OPT_PREFILL_ATTN_SPLIT = 6
 
 # enum xh_tensor_kind
 EMBED, ATTN_NORM, FFN_NORM, WQ, WK, WV, WO, W1, W2, W3, FINAL_NORM, WCLS = range(12)

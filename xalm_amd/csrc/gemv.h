@@ -31,7 +31,7 @@ enum { EPI_STORE = 0, EPI_RESID = 1, EPI_QKV = 2, EPI_GLU = 3, EPI_LOGITS = 4 };
 constexpr int LDS_HEAD_BYTES = 64;  // block-reduction scratch in front of the x image
 
 // attn_wo.h hand-off words of a layer that the launch after it zeroes (every 32nd word)
-constexpr int AW_RESET_WORDS = 9;
+constexpr int AW_RESET_WORDS = 17;
 
 // Launch shape of one gemv instance.
 template <int THREADS_, int ROWS_, int U_, bool NT_ = true, int MINW_ = 4, bool PF_ = true, int XN_ = 0, int PIPE_ = 1>

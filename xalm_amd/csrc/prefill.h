@@ -912,9 +912,16 @@ __device__ __forceinline__ uint32_t fa_off(const int r, const int c) {
 }
 typedef short fa_s16x4 __attribute__((ext_vector_type(4)));
 
+// History split (grid z = nsplit > 1, a pass too short to fill the chip over a long history):
+// workgroup z walks ring stages [z H / nsplit, (z + 1) H / nsplit) with H = pos0 / 64 (the last
+// split runs to the workgroup's last slot), so every split starts at a slot <= pos0 <= each
+// row's pos and its first tile has a finite max; it writes its unnormalised O and (m, l) to
+// part_o [z][n][q_stride] / part_ml [z][n][n_heads], and prefill_fa_merge_kernel combines the
+// splits in split order (deterministic).
 template <int QPK, int NW>
 __global__ __launch_bounds__(64 * NW, 2) void prefill_fa2_kernel(const float* q, const uint16_t* kc, const uint16_t* vc,
-                                                               float* out, int n, int pos0, int q_stride, int kv_dim) {
+                                                               float* out, int n, int pos0, int q_stride, int kv_dim,
+                                                               float* part_o, float2* part_ml) {
     constexpr int HD = 128;
     constexpr int TPW = 32 / QPK;        // tokens per wave
     constexpr int KS = HD / 16;          // k steps of q . k
@@ -946,13 +953,17 @@ __global__ __launch_bounds__(64 * NW, 2) void prefill_fa2_kernel(const float* q,
         dch[k] = (lane & 15) ^ (((r & 3) << 2) | ((r >> 2) & 3));
     }
     const int ntile = last_wg / 32 + 1;
-    const int nst = (ntile + FA_TPS - 1) / FA_TPS;
+    const int nst_all = (ntile + FA_TPS - 1) / FA_TPS;
+    const int nsplit = gridDim.z, z = blockIdx.z;
+    const int hst = pos0 / (32 * FA_TPS);  // stage boundaries at or below pos0
+    const int st0 = nsplit > 1 ? z * hst / nsplit : 0;
+    const int nst = (nsplit > 1 && z < nsplit - 1 ? (z + 1) * hst / nsplit : nst_all) - st0;
     auto issue = [&](const int stage, const int st) {
         char* base = fa_smem + stage * FA_STAGE_BYTES;
 #pragma unroll
         for (int k = 0; k < IPW; k++) {
             const int i = wv * IPW + k;
-            const uint16_t* src = (((i >> 3) & 1) ? vc : kc) + (size_t)min(32 * FA_TPS * st + drow[k], last_wg) * kv_dim +
+            const uint16_t* src = (((i >> 3) & 1) ? vc : kc) + (size_t)min(32 * FA_TPS * (st0 + st) + drow[k], last_wg) * kv_dim +
                                   (size_t)g * HD + 8 * dch[k];
             __builtin_amdgcn_global_load_lds((const void*)src,
                                              (__attribute__((address_space(3))) void*)(base + i * 1024), 16, 0, 0);
@@ -1009,7 +1020,7 @@ __global__ __launch_bounds__(64 * NW, 2) void prefill_fa2_kernel(const float* q,
         if (ks + FA_NS - 1 < nst) issue((ks + FA_NS - 1) % FA_NS, ks + FA_NS - 1);
 #pragma unroll
         for (int sub = 0; sub < FA_TPS; sub++) {
-        const int b = 32 * (ks * FA_TPS + sub);
+        const int b = 32 * ((st0 + ks) * FA_TPS + sub);
         if (b > last) break;  // wave-uniform: past this wave's rows (it still issues its DMA share)
         const char* kimg = fa_smem + (ks % FA_NS) * FA_STAGE_BYTES + sub * 2 * FA_TILE_BYTES;
         const char* vimg = kimg + FA_TILE_BYTES;
@@ -1045,8 +1056,10 @@ __global__ __launch_bounds__(64 * NW, 2) void prefill_fa2_kernel(const float* q,
     }
     const float l = lsum + __shfl_xor(lsum, 32);
     if (tq >= n) return;
-    const float inv_l = 1.f / l;
-    float* orow = out + (size_t)tq * q_stride + (size_t)head * HD;
+    const bool split = nsplit > 1;
+    const float inv_l = split ? 1.f : 1.f / l;
+    float* orow = (split ? part_o + (size_t)z * n * q_stride : out) + (size_t)tq * q_stride + (size_t)head * HD;
+    if (split && h == 0) part_ml[((size_t)z * n + tq) * (q_stride / HD) + head] = float2{m, l};
 #pragma unroll
     for (int dt = 0; dt < NDT; dt++)
 #pragma unroll
@@ -1055,6 +1068,31 @@ __global__ __launch_bounds__(64 * NW, 2) void prefill_fa2_kernel(const float* q,
             *(float4*)(orow + d) =
                 float4{o[dt][r] * inv_l, o[dt][r + 1] * inv_l, o[dt][r + 2] * inv_l, o[dt][r + 3] * inv_l};
         }
+}
+
+// the history splits of prefill_fa2_kernel combined per (token, head), in split order:
+// M = max m_z, out = sum_z e^(m_z - M) o_z / sum_z e^(m_z - M) l_z.  grid (n), 256 threads, one
+// float4 of a row per thread-iteration; HD = 128.
+__global__ __launch_bounds__(256) void prefill_fa_merge_kernel(const float* part_o, const float2* part_ml, float* out,
+                                                               int n, int nsplit, int q_stride) {
+    const int t = blockIdx.x;
+    const int nh = q_stride / 128;
+    for (int i = threadIdx.x; i < q_stride / 4; i += 256) {
+        const int head = (4 * i) / 128;
+        float mx = -INFINITY;
+        for (int z = 0; z < nsplit; z++) mx = fmaxf(mx, part_ml[((size_t)z * n + t) * nh + head].x);
+        float4 acc = float4{0.f, 0.f, 0.f, 0.f};
+        float l = 0.f;
+        for (int z = 0; z < nsplit; z++) {
+            const float2 ml = part_ml[((size_t)z * n + t) * nh + head];
+            const float w = __expf(ml.x - mx);
+            const float4 v = *(const float4*)(part_o + ((size_t)z * n + t) * q_stride + 4 * i);
+            l += w * ml.y;
+            acc.x += w * v.x; acc.y += w * v.y; acc.z += w * v.z; acc.w += w * v.w;
+        }
+        const float inv_l = 1.f / l;
+        *(float4*)(out + (size_t)t * q_stride + 4 * i) = float4{acc.x * inv_l, acc.y * inv_l, acc.z * inv_l, acc.w * inv_l};
+    }
 }
 
 // fp8 weights (e4m3 / e5m2, finite codes only: the _EXACT dtypes never come here) -> f16 bits

@@ -150,6 +150,7 @@ struct xh_ctx {
     bool pf_split_ready = false;                 // pf_norm left the next GEMM's split input
     bool pf_resid_norm = true;                   // residual + rmsnorm split in one launch (XH_OPT_PREFILL_GLU_SPLIT 0: off)
     bool pf_glu_split = true;                    // XH_OPT_PREFILL_GLU_SPLIT: fused GLU -> split input
+    int pf_fa_split = 1;                         // XH_OPT_PREFILL_ATTN_SPLIT: history splits for short passes
     int pf_attn_mode = 1;                        // XH_OPT_PREFILL_ATTN: 1 shared-tile MFMA (v1 for head_dim != 128),
                                                  // 2 per-wave MFMA tiles, 0 per-token split kernel
     // T = pf_cap tokens (the pass length in use; pf_alloc)
@@ -1133,6 +1134,19 @@ void pf_attn_t(xh_ctx* ctx, const AttnArgs& a, int n) {
     hipLaunchKernelGGL(k, dim3(ctx->c.n_kv_heads, a.nsplit, n), dim3(ATTN_THREADS), smem, ctx->stream, a,
                        (const StepParams*)ctx->pf_sp, ctx->q_dim, ctx->c.n_kv_heads);
 }
+// History splits of the shared-tile prompt attention: a pass whose (KV head, query tile)
+// workgroups cannot fill two per CU (a short pass: 8 workgroups for <= 32 tokens at 8 KV heads)
+// walks its history in up to that many splits of >= FA_MIN_SPLIT_STAGES ring stages each (the
+// split partials live in pf_part, free between the qkv epilogue and the Wo GEMM).
+constexpr int FA_MIN_SPLIT_STAGES = 4;
+int pf_fa_nsplit(const xh_ctx* ctx, int nqt, int n, int pos0) {
+    if (!ctx->pf_fa_split) return 1;
+    const int wg = ctx->c.n_kv_heads * nqt;
+    int ns = std::min((2 * ctx->n_cu + wg - 1) / wg, pos0 / (32 * FA_TPS) / FA_MIN_SPLIT_STAGES);
+    const size_t per = (size_t)n * (ctx->q_dim + 2 * ctx->c.n_heads);
+    ns = (int)std::min<size_t>((size_t)ns, pf_part_floats(ctx, ctx->pf_cap) / per);
+    return std::max(ns, 1);
+}
 template <int HD, int QPK>
 void pf_fa_t(xh_ctx* ctx, const AttnArgs& a, int n, int pos0) {
     constexpr int TPW = 32 / QPK;
@@ -1141,8 +1155,15 @@ void pf_fa_t(xh_ctx* ctx, const AttnArgs& a, int n, int pos0) {
             constexpr int NW = PF_FA_WAVES;
             auto k = prefill_fa2_kernel<QPK, NW>;
             ensure_lds((const void*)k);
-            hipLaunchKernelGGL(k, dim3(ctx->c.n_kv_heads, (n + NW * TPW - 1) / (NW * TPW)), dim3(64 * NW),
-                               fa_lds_bytes(), ctx->stream, a.q, a.kc, a.vc, a.out, n, pos0, ctx->q_dim, ctx->kv_dim);
+            const int nqt = (n + NW * TPW - 1) / (NW * TPW);
+            const int nsplit = pf_fa_nsplit(ctx, nqt, n, pos0);
+            float* po = nsplit > 1 ? ctx->pf_part : nullptr;
+            float2* pml = nsplit > 1 ? (float2*)(ctx->pf_part + (size_t)nsplit * n * ctx->q_dim) : nullptr;
+            hipLaunchKernelGGL(k, dim3(ctx->c.n_kv_heads, nqt, nsplit), dim3(64 * NW), fa_lds_bytes(), ctx->stream, a.q,
+                               a.kc, a.vc, a.out, n, pos0, ctx->q_dim, ctx->kv_dim, po, pml);
+            if (nsplit > 1)
+                hipLaunchKernelGGL(prefill_fa_merge_kernel, dim3(n), dim3(256), 0, ctx->stream, (const float*)po,
+                                   (const float2*)pml, a.out, n, nsplit, ctx->q_dim);
             return;
         }
     }
@@ -2027,6 +2048,7 @@ int xh_get_option(const xh_ctx* ctx, int option, int* value) {
         case XH_OPT_PREFILL: *value = ctx->prefill_batched ? ctx->prefill_gemm : 0; return 0;
         case XH_OPT_PREFILL_GLU_SPLIT: *value = ctx->pf_glu_split ? 1 : 0; return 0;
         case XH_OPT_PREFILL_ATTN: *value = ctx->pf_attn_mode; return 0;
+        case XH_OPT_PREFILL_ATTN_SPLIT: *value = ctx->pf_fa_split; return 0;
         default: return XH_E_INVALID;
     }
 }
@@ -2052,6 +2074,10 @@ int xh_set_option(xh_ctx* ctx, int option, int value) {
         case XH_OPT_PREFILL_ATTN:
             if (value < 0 || value > 2) return set_err(ctx, XH_E_INVALID, "XH_OPT_PREFILL_ATTN: 0, 1 or 2");
             ctx->pf_attn_mode = value;
+            return 0;
+        case XH_OPT_PREFILL_ATTN_SPLIT:
+            if (value < 0 || value > 1) return set_err(ctx, XH_E_INVALID, "XH_OPT_PREFILL_ATTN_SPLIT: 0 or 1");
+            ctx->pf_fa_split = value;
             return 0;
         default: return set_err(ctx, XH_E_INVALID, "unknown option %d", option);
     }
