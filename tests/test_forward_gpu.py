@@ -140,7 +140,7 @@ def test_prefill_matches_oracle(name, context, engine):
 
 @pytest.mark.parametrize("mode", [1, 2, 3, 4])
 @pytest.mark.parametrize("name", FIXTURES)
-@pytest.mark.parametrize("n", [1, 37, 64, 150])
+@pytest.mark.parametrize("n", [2, 37, 64, 150])
 def test_batched_prefill_matches_oracle(name, n, mode):
     """xh_prefill's batched path (prefill.h / gemm16.h: the LDS-tiled f16 MFMA GEMM over passes of
     <= PF_TOK_MM = 2048 tokens for f16 / fp8 weights, register-streaming MFMA GEMMs over passes of <= 64 tokens

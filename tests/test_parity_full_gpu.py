@@ -57,11 +57,6 @@ def gpu_side(w, c, shift=0):
                 gm.kv_fill_synthetic(layer, 0, 0, hist, 5000 + 2 * layer, 1.0)
                 gm.kv_fill_synthetic(layer, 1, 0, hist, 5001 + 2 * layer, 1.0)
         fill()
-        # the one-token hydrate through the batched prompt path too (the prompt attention's
-        # history splits: 8 workgroups' worth of work spread over the chip); it writes slot hist,
-        # which the token loop below rewrites
-        gm.prefill(prompt[:1], hist, st)
-        out["prefill"] = st.logits().copy()
         gm.forward(st, prompt[0], hist, L.OUTPUT_LOGITS)
         out["loop"] = st.logits().copy()
         toks = gm.decode_greedy(hist + 1, DECODE)

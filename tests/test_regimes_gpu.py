@@ -439,12 +439,12 @@ def test_prompt_over_long_history(attn, split):
     om.close()
 
 
-@pytest.mark.parametrize("n", [1, 32, 256])
+@pytest.mark.parametrize("n", [1, 2, 32, 256])
 def test_short_prompt_over_32k_history(n):
     """Short prompt passes over a ~32.7k-slot history at configs[3]'s head shape (32 q heads, 8 KV
     heads, head_dim 128; src/main.cpp:94-100 resuming a long chat): a pass of n tokens has
     8 * ceil(n / 32) (KV head, query tile) workgroups, so XH_OPT_PREFILL_ATTN_SPLIT 1 walks the
-    history in up to 64 splits merged in split order.  Both the split and the single-walk forms
+    history in up to 64 splits merged in split order (n = 1 takes the decode step instead).  Both the split and the single-walk forms
     against the oracle's token loop (last logits, the pass's K/V rows), and the split form
     repeatable bit for bit (fixed merge order)."""
     c = make_cfg(256, 512, 2, 32, 8, 128, 512, 32768)

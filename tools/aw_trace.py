@@ -15,6 +15,8 @@ def main():
     ap.add_argument("--workload", default="mistral-7b-f16")
     ap.add_argument("--fuse", type=int, default=1, help="XH_OPT_FUSE_ATTN_WO (2: W1/W3 role traced too)")
     ap.add_argument("--aw-threads", type=int, default=1024, help="AW_THREADS of the library (XALM_HIP_LIB)")
+    ap.add_argument("--pos0", type=int, default=0, help="4k workloads: synthetic K/V history [0, pos0) first "
+                    "(e.g. 3800: the traced token attends over ~4k slots)")
     args = ap.parse_args()
     w = bench.WORKLOADS[args.workload]
     c = bench.make_config(w)
@@ -34,9 +36,12 @@ def main():
         m.prefill(prompt[:1], pos, st)
         pos += 1
     else:
-        m.prefill(prompt, 0, st)
-        m.decode_greedy(len(prompt), 200)
-        pos = len(prompt) + 200
+        for layer in range(c.n_layers if args.pos0 else 0):
+            m.kv_fill_synthetic(layer, 0, 0, args.pos0, 5000 + 2 * layer, 1.0)
+            m.kv_fill_synthetic(layer, 1, 0, args.pos0, 5001 + 2 * layer, 1.0)
+        m.prefill(prompt, args.pos0, st)
+        m.decode_greedy(args.pos0 + len(prompt), 200)
+        pos = args.pos0 + len(prompt) + 200
     m.debug_trace(2)
     m.decode_greedy(pos, 2)
     tr = m.debug_trace(0).astype(np.int64)

@@ -39,12 +39,8 @@ using AwShape = GemvShape<AW_THREADS, 2, (WDec<DT>::E >= 16 ? 4 : 8), true, 4, t
 // XCD's Wo workgroups (one polled line per XCD instead of every Wo workgroup polling the
 // counter the arrivals add to).  Words 0, 32, ..., 32 (AW_RESET_WORDS - 1) are zeroed by the
 // next launch.
-// [AW_ISS0 + 32 k]: attention workgroups that have requested their first K/V round, counted per
-// XCD k (every attention workgroup adds 1 to all 8; AW_HOLD: a Wo workgroup requests its rows only
-// once its XCD's count is complete, so the K/V requests are not queued behind the Wo stream).
 constexpr int AW_FLAG0 = 32;
-constexpr int AW_ISS0 = AW_FLAG0 + 8 * 32;
-constexpr int AW_SYNC_WORDS = AW_ISS0 + 8 * 32;
+constexpr int AW_SYNC_WORDS = AW_FLAG0 + 8 * 32;
 static_assert(AW_SYNC_WORDS == 32 * AW_RESET_WORDS, "every hand-off word is reset");
 
 // More than MAXS partials per head to merge (aw_stage_merged keeps MAXS in registers beside
@@ -54,21 +50,6 @@ constexpr int AW_MAXS = 4;
 #ifndef AW_EARLY_WAVE0
 #define AW_EARLY_WAVE0 1
 #endif
-#ifndef AW_HOLD
-#define AW_HOLD 0  // 1: Wo rows requested after every active attention split issued its K/V loads
-#endif
-#ifndef AW_FIRST
-#define AW_FIRST 0  // > 0: Wo chunks requested before a wait for them, the rest after (0: all at once)
-#endif
-// attention side of AW_HOLD: after the first K/V round is requested, count this workgroup on
-// every XCD's issue counter (no return value: nothing waits on it)
-struct AwIssued {
-    unsigned* sync;
-    __device__ void operator()() const {
-        if (threadIdx.x < 8)
-            __hip_atomic_fetch_add(sync + AW_ISS0 + 32 * threadIdx.x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-};
 template <int HD>
 __device__ __forceinline__ bool aw_long(const AttnArgs& aa) {
     const int kv_len = aa.sp->kv_len;
@@ -218,20 +199,13 @@ __global__ __launch_bounds__(AW_THREADS) void attn_wo_kernel(const AttnArgs aa, 
                     __hip_atomic_store(c + AW_FLAG0 + 32 * k, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
         };
-#if AW_HOLD
-        using IssueHook = AwIssued;
-        const IssueHook hook{sync};
-#else
-        using IssueHook = NoWait;
-        const IssueHook hook{};
-#endif
         if (merged) {
             // long contexts: each KV head's last split merges (ticket) and signals the head
-            attn_block<HD, QPK, AW_THREADS, false, attn_min_t_partials(HD, AW_THREADS), IssueHook,
-                       decltype(arrive), true>(aa, g, s, smem, sync, nullptr, hook, arrive);
+            attn_block<HD, QPK, AW_THREADS, false, attn_min_t_partials(HD, AW_THREADS), NoWait,
+                       decltype(arrive), true>(aa, g, s, smem, sync, nullptr, NoWait(), arrive);
         } else {
-            attn_block<HD, QPK, AW_THREADS, true, 0, IssueHook, decltype(arrive)>(
-                aa, g, s, smem, sync, trace ? trace + 8 * b : nullptr, hook, arrive);
+            attn_block<HD, QPK, AW_THREADS, true, 0, NoWait, decltype(arrive)>(
+                aa, g, s, smem, sync, trace ? trace + 8 * b : nullptr, NoWait(), arrive);
         }
         if (trace && threadIdx.x == 0) trace[8 * b + 1] = __builtin_amdgcn_s_memrealtime();
         return;
@@ -270,20 +244,7 @@ __global__ __launch_bounds__(AW_THREADS) void attn_wo_kernel(const AttnArgs aa, 
         u32x4 w[S::U][S::ROWS];
         float xres[S::ROWS];
         auto fetch = [&]() {
-            if constexpr (AW_FIRST > 0 && AW_FIRST < S::U) {
-                size_t rs;
-                const char* wrow = gemv_row_ptr<S::ROWS>(ga, g, lane, rs);
-#pragma unroll
-                for (int u = 0; u < S::U; u++) {
-                    if (u == AW_FIRST) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-                    for (int r = 0; r < S::ROWS; r++)
-                        w[u][r] = __builtin_nontemporal_load(
-                            (const __attribute__((address_space(1))) u32x4*)(wrow + (size_t)r * rs + (size_t)u * 1024));
-                }
-            } else {
-                gemv_prefetch<S>(ga, g, lane, w);
-            }
+            gemv_prefetch<S>(ga, g, lane, w);
             if (lane == 0) {
 #pragma unroll
                 for (int r = 0; r < S::ROWS; r++) xres[r] = g * S::ROWS + r < ga.rows ? ga.out[g * S::ROWS + r] : 0.f;
@@ -294,20 +255,6 @@ __global__ __launch_bounds__(AW_THREADS) void attn_wo_kernel(const AttnArgs aa, 
         // full HBM rate) before the heads are done, while rows requested after the hand-off
         // made wave 0 the launch's last wave by ≈1.5 µs
         const bool early = AW_EARLY_WAVE0 || wid != 0;
-#if AW_HOLD
-        if (threadIdx.x == 0) {
-            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-            int xcc;
-            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 3)" : "=s"(xcc));
-            const unsigned* cnt = sync + AW_ISS0 + 32 * (xcc & 7);
-            const unsigned n_iss = (unsigned)(n_kv_heads * n_active);
-            while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < n_iss) {
-                __builtin_amdgcn_s_sleep(1);
-                if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) break;  // 2 s: go on (a hint only)
-            }
-        }
-        __syncthreads();
-#endif
         if (g < n_groups && early) fetch();
         wait_heads();
         if (g < n_groups && !early) fetch();

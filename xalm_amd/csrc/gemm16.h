@@ -383,8 +383,11 @@ __global__ __launch_bounds__(64 * NW, OCC) void mm_f16_kernel_t(const MmArgs a) 
 // the product's instantiations: the default, and for launches of >= MM_W4_PER_CU workgroups per
 // CU (W1/W3 and the lm_head at 2048 tokens) two 4-wave workgroups per CU with 32-deep steps in
 // 64 KiB each, every wave 64 tokens x 128 rows (tools/gemm_bench, 2048 tokens: W1/W3 840 -> 809
-// us; qkv, Wo, W2 slower, their launches have 1-3 workgroups per CU).  Same k order per
-// accumulator (32-deep MFMA steps, hi then lo), so the same bits as the default.
+// us; qkv, Wo, W2 slower, their launches have 1-3 workgroups per CU).  Inside a K slice both
+// sum each accumulator in the same k order (32-deep MFMA steps, hi then lo); the K-slice count
+// is picked per instantiation (mm_pick_ks with its token tile), so the two can differ in the
+// last bits of a partial sum.  Which one runs depends on the launch's workgroups per CU (the
+// device's CU count): tests compare either against the float64 product, not against each other.
 #define mm_f16_kernel mm_f16_kernel_t<MM_BK, MM_NS, MM_FL, MM_BT>
 #define mm_f16_kernel_w4 mm_f16_kernel_t<32, 2, MM_FL, MM_BT, 2, 4>
 constexpr int MM_LDS_W4 = MmCfg<32, 2, MM_BT, 4>::LDS;

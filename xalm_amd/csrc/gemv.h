@@ -31,7 +31,7 @@ enum { EPI_STORE = 0, EPI_RESID = 1, EPI_QKV = 2, EPI_GLU = 3, EPI_LOGITS = 4 };
 constexpr int LDS_HEAD_BYTES = 64;  // block-reduction scratch in front of the x image
 
 // attn_wo.h hand-off words of a layer that the launch after it zeroes (every 32nd word)
-constexpr int AW_RESET_WORDS = 17;
+constexpr int AW_RESET_WORDS = 9;
 
 // Launch shape of one gemv instance.
 template <int THREADS_, int ROWS_, int U_, bool NT_ = true, int MINW_ = 4, bool PF_ = true, int XN_ = 0, int PIPE_ = 1>
@@ -271,7 +271,6 @@ __device__ __forceinline__ void gemv_epilogue(const GemvArgs& a, const int row0,
 #pragma unroll
         for (int p = 0; p < ROWS; p += 2) epi_st<SC1>(a.out + ((row0 + p) >> 1), act_fn(a.act, acc[p]) * acc[p + 1]);
     } else {  // EPI_QKV
-        const int pos = pre ? pre->pos : a.sp->pos;
         const int kv_pos = pre ? pre->kv_pos : a.sp->kv_pos;
 #pragma unroll
         for (int p = 0; p < ROWS; p += 2) {
@@ -428,28 +427,6 @@ __device__ __forceinline__ float gq_dot(const u32x4 w, const float4* xv) {
     } else {
         // Q4_0: byte j = element j (low nibble) | element j + 16 (high); 1024 + n - 1032 = n - 8
         const h2_t c = __builtin_bit_cast(h2_t, 0xE408E408u);
-#if defined(GQ_HIMASK)
-        // high nibbles masked in place (no shift): under the f16 exponent of 2^14 the byte 16 n
-        // reads 16384 + 256 n; minus 18432 = 256 (n - 8), exact; that sum is scaled by 2^-8
-        const h2_t ch = __builtin_bit_cast(h2_t, 0xF480F480u);
-        float sh = 0.f;
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-            const uint32_t lo = ww[i] & 0x0F0F0F0Fu, hm = ww[i] & 0xF0F0F0F0u;
-            const uint32_t l01 = gq_pair(lo, 0x04010400u, c), l23 = gq_pair(lo, 0x04030402u, c);
-            const uint32_t h01 = __builtin_bit_cast(uint32_t, __builtin_bit_cast(h2_t, __builtin_amdgcn_perm(0x74747474u, hm, 0x04010400u)) + ch);
-            const uint32_t h23 = __builtin_bit_cast(uint32_t, __builtin_bit_cast(h2_t, __builtin_amdgcn_perm(0x74747474u, hm, 0x04030402u)) + ch);
-            s = fma_mix_lo(l01, xv[i].x, s);
-            s = fma_mix_hi(l01, xv[i].y, s);
-            s = fma_mix_lo(l23, xv[i].z, s);
-            s = fma_mix_hi(l23, xv[i].w, s);
-            sh = fma_mix_lo(h01, xv[4 + i].x, sh);
-            sh = fma_mix_hi(h01, xv[4 + i].y, sh);
-            sh = fma_mix_lo(h23, xv[4 + i].z, sh);
-            sh = fma_mix_hi(h23, xv[4 + i].w, sh);
-        }
-        return fmaf(sh, 0x1p-8f, s);
-#endif
 #pragma unroll
         for (int i = 0; i < 4; i++) {
             const uint32_t lo = ww[i] & 0x0F0F0F0Fu, hi = (ww[i] >> 4) & 0x0F0F0F0Fu;

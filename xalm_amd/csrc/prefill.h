@@ -311,7 +311,7 @@ __global__ __launch_bounds__(256) void prefill_resid_norm_split_kernel(const flo
                                                                        float* x, int dim, const void* w, int wdt,
                                                                        float eps, int n, int E, uint16_t* xh,
                                                                        uint16_t* xl, float* inv_s) {
-    extern __shared__ float xrow[];
+    extern __shared__ __attribute__((aligned(16))) float xrow[];  // float4 reads and writes
     __shared__ float red[4];
     const int t = blockIdx.x;
     auto frag = [&](const int k) { return split_off(t, k, dim, E); };
@@ -1070,28 +1070,51 @@ __global__ __launch_bounds__(64 * NW, 2) void prefill_fa2_kernel(const float* q,
         }
 }
 
-// the history splits of prefill_fa2_kernel combined per (token, head), in split order:
-// M = max m_z, out = sum_z e^(m_z - M) o_z / sum_z e^(m_z - M) l_z.  grid (n), 256 threads, one
-// float4 of a row per thread-iteration; HD = 128.
+// the history splits of prefill_fa2_kernel combined per (token, head), in a fixed order:
+// M = max m_z, out = sum_z e^(m_z - M) o_z / sum_z e^(m_z - M) l_z.  grid (n_heads, n), 256
+// threads = 32 float4 columns of the head (HD = 128) x 8 split groups; group k takes splits
+// k, k + 8, ... (its loads issued together), the 8 group sums are added in group order.
+constexpr int FA_MERGE_GROUPS = 8;
 __global__ __launch_bounds__(256) void prefill_fa_merge_kernel(const float* part_o, const float2* part_ml, float* out,
                                                                int n, int nsplit, int q_stride) {
-    const int t = blockIdx.x;
-    const int nh = q_stride / 128;
-    for (int i = threadIdx.x; i < q_stride / 4; i += 256) {
-        const int head = (4 * i) / 128;
-        float mx = -INFINITY;
-        for (int z = 0; z < nsplit; z++) mx = fmaxf(mx, part_ml[((size_t)z * n + t) * nh + head].x);
-        float4 acc = float4{0.f, 0.f, 0.f, 0.f};
-        float l = 0.f;
-        for (int z = 0; z < nsplit; z++) {
-            const float2 ml = part_ml[((size_t)z * n + t) * nh + head];
-            const float w = __expf(ml.x - mx);
-            const float4 v = *(const float4*)(part_o + ((size_t)z * n + t) * q_stride + 4 * i);
-            l += w * ml.y;
-            acc.x += w * v.x; acc.y += w * v.y; acc.z += w * v.z; acc.w += w * v.w;
+    constexpr int G = FA_MERGE_GROUPS;
+    __shared__ float smax[G];
+    __shared__ float4 snum[G][32];
+    __shared__ float sden[G];
+    const int head = blockIdx.x, t = blockIdx.y;
+    const int nh = gridDim.x;
+    const int c = threadIdx.x & 31, k = threadIdx.x >> 5;
+    auto ml_at = [&](const int z) { return part_ml[((size_t)z * n + t) * nh + head]; };
+    float mx = -INFINITY;
+    for (int z = k; z < nsplit; z += G) mx = fmaxf(mx, ml_at(z).x);
+    if (c == 0) smax[k] = mx;
+    __syncthreads();
+    float M = smax[0];
+#pragma unroll
+    for (int i = 1; i < G; i++) M = fmaxf(M, smax[i]);
+    float4 acc = float4{0.f, 0.f, 0.f, 0.f};
+    float l = 0.f;
+    for (int z = k; z < nsplit; z += G) {
+        const float2 m_l = ml_at(z);
+        const float w = __expf(m_l.x - M);
+        const float4 v = *(const float4*)(part_o + ((size_t)z * n + t) * q_stride + (size_t)head * 128 + 4 * c);
+        l += w * m_l.y;
+        acc.x += w * v.x; acc.y += w * v.y; acc.z += w * v.z; acc.w += w * v.w;
+    }
+    snum[k][c] = acc;
+    if (c == 0) sden[k] = l;
+    __syncthreads();
+    if (k == 0) {
+        float4 s4 = snum[0][c];
+        float den = sden[0];
+#pragma unroll
+        for (int i = 1; i < G; i++) {
+            s4.x += snum[i][c].x; s4.y += snum[i][c].y; s4.z += snum[i][c].z; s4.w += snum[i][c].w;
+            den += sden[i];
         }
-        const float inv_l = 1.f / l;
-        *(float4*)(out + (size_t)t * q_stride + 4 * i) = float4{acc.x * inv_l, acc.y * inv_l, acc.z * inv_l, acc.w * inv_l};
+        const float inv_l = 1.f / den;
+        *(float4*)(out + (size_t)t * q_stride + (size_t)head * 128 + 4 * c) =
+            float4{s4.x * inv_l, s4.y * inv_l, s4.z * inv_l, s4.w * inv_l};
     }
 }
 

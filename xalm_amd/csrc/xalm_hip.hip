@@ -1103,22 +1103,25 @@ void pf_epi(xh_ctx* ctx, PfEpiArgs e);
 // x += the last GEMM's partials (EPI_RESID), then the rmsnorm of the updated rows as the input of
 // the GEMM over W (dt, [rows][dim]): one launch when that GEMM takes the split input and the
 // rows fit the LDS, else pf_epi + pf_norm (the same bits either way)
-void pf_resid_norm(xh_ctx* ctx, int ks, const void* nw, int ndt, int m, int dt, int rows) {
+int pf_resid_norm(xh_ctx* ctx, int ks, const void* nw, int ndt, int m, int dt, int rows) {
     const xh_config& c = ctx->c;
     const int lay = pf_layout(ctx, dt, c.dim, rows);
-    const size_t lds = (size_t)c.dim * sizeof(float);
-    if (lay >= 0 && ctx->pf_resid_norm && c.dim % 8 == 0 && lds <= 64 * 1024) {
+    const size_t lds = (size_t)c.dim * sizeof(float);  // + the kernel's static red[4]
+    if (lay >= 0 && ctx->pf_resid_norm && c.dim % 8 == 0 && lds + 4 * sizeof(float) <= 64 * 1024) {
+        HIP_TRY(ctx, hipGetLastError());  // an earlier launch's error is reported as such
         hipLaunchKernelGGL(prefill_resid_norm_split_kernel, dim3(pf_split_grid(lay, m)), dim3(256), lds, ctx->stream,
                            (const float*)ctx->pf_part, ks, (const float*)(ctx->pf_scaled ? ctx->pf_xs : nullptr),
                            ctx->pf_x, c.dim, nw, ndt, c.norm_eps, m, lay, ctx->pf_xh, pf_lo(ctx, lay, m, c.dim),
                            ctx->pf_xs);
+        HIP_TRY(ctx, hipGetLastError());
         ctx->pf_split_ready = true;
-        return;
+        return 0;
     }
     PfEpiArgs e{};
     e.ks = ks; e.n = m; e.rows = c.dim; e.epi = EPI_RESID; e.out = ctx->pf_x;
     pf_epi(ctx, e);
     pf_norm(ctx, nw, ndt, m, dt, rows);
+    return 0;
 }
 void pf_epi(xh_ctx* ctx, PfEpiArgs e) {
     e.part = ctx->pf_part;
@@ -1162,7 +1165,7 @@ void pf_fa_t(xh_ctx* ctx, const AttnArgs& a, int n, int pos0) {
             hipLaunchKernelGGL(k, dim3(ctx->c.n_kv_heads, nqt, nsplit), dim3(64 * NW), fa_lds_bytes(), ctx->stream, a.q,
                                a.kc, a.vc, a.out, n, pos0, ctx->q_dim, ctx->kv_dim, po, pml);
             if (nsplit > 1)
-                hipLaunchKernelGGL(prefill_fa_merge_kernel, dim3(n), dim3(256), 0, ctx->stream, (const float*)po,
+                hipLaunchKernelGGL(prefill_fa_merge_kernel, dim3(ctx->c.n_heads, n), dim3(256), 0, ctx->stream, (const float*)po,
                                    (const float2*)pml, a.out, n, nsplit, ctx->q_dim);
             return;
         }
@@ -1281,7 +1284,7 @@ int prefill_batched(xh_ctx* ctx, const int* tokens, int n, int pos0, int want_lo
             if ((rc = pf_attn(ctx, aa, m, p0))) return rc;
             if ((rc = pf_gemm(ctx, "wo", kdt(w.wo_dt, w.wo_x), w.wo, ctx->q_dim, c.dim, ctx->pf_att, m, ks))) return rc;
             // residual, then the feed-forward block's rmsnorm (src/infer.cpp:449-452, 455-494)
-            pf_resid_norm(ctx, ks, w.ffn_norm, w.fn_dt, m, kdt(w.w13_dt, w.w13_x), 2 * c.hidden_dim);
+            if ((rc = pf_resid_norm(ctx, ks, w.ffn_norm, w.fn_dt, m, kdt(w.w13_dt, w.w13_x), 2 * c.hidden_dim))) return rc;
             if ((rc = pf_gemm(ctx, "w1/w3", kdt(w.w13_dt, w.w13_x), w.w13, c.dim, 2 * c.hidden_dim, ctx->pf_xn, m, ks)))
                 return rc;
             const int lay2 = pf_layout(ctx, kdt(w.w2_dt, w.w2_x), c.hidden_dim, c.dim);
@@ -1311,7 +1314,7 @@ int prefill_batched(xh_ctx* ctx, const int* tokens, int n, int pos0, int want_lo
             if (l + 1 < c.n_layers) {
                 // residual, then the next layer's attention rmsnorm (src/infer.cpp:491-494, 380)
                 const LayerW& wn = ctx->L[l + 1];
-                pf_resid_norm(ctx, ks, wn.attn_norm, wn.an_dt, m, kdt(wn.qkv_dt, wn.qkv_x), qkv_rows);
+                if ((rc = pf_resid_norm(ctx, ks, wn.attn_norm, wn.an_dt, m, kdt(wn.qkv_dt, wn.qkv_x), qkv_rows))) return rc;
             } else {
                 e = PfEpiArgs{};
                 e.ks = ks; e.n = m; e.rows = c.dim; e.epi = EPI_RESID; e.out = ctx->pf_x;
@@ -1966,7 +1969,9 @@ int xh_prefill(xh_ctx* ctx, const int* tokens, int n, int pos0, int want_logits,
     HIP_TRY(ctx, hipSetDevice(ctx->dev));
     int rc = check_ready(ctx);
     if (rc) return rc;
-    if (pf_supported(ctx, n, pos0)) {
+    // a one-token prompt runs the decode step (one graph replay of the matvecs) rather than a
+    // pass of GEMMs over one token: 3.3 vs 7.3 ms at the end of a 32k ring (tools/short_pass.py)
+    if (n >= 2 && pf_supported(ctx, n, pos0)) {
         rc = prefill_batched(ctx, tokens, n, pos0, want_logits);
     } else {
         for (int i = 0; i < n && !rc; i++) {
