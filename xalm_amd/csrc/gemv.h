@@ -177,10 +177,29 @@ __device__ __forceinline__ float4 load_norm4_nb(const void* w, const int dtype, 
                        bf ? bits_f32(u.y << 16) : bits_f32(u.z), bf ? bits_f32(u.y & 0xffff0000u) : bits_f32(u.w));
 }
 
+// Q4_0 staging (the denormal form of gq_dot): the image holds x / 16 for elements 16..31 of each
+// 32-element block and, after the n_it * 64 * E floats of the image, -8 sum(x) of every block
+template <int DT>
+__device__ __host__ constexpr bool gq4_image() { return DT == XH_Q4_0; }
+__device__ __forceinline__ const float* gq4_nxs(const float4* xs4, const int n) {
+    constexpr int E = 32;
+    return (const float*)xs4 + (size_t)((n + 64 * E - 1) / (64 * E)) * 64 * E;
+}
+// one float4 v = x[4 i .. 4 i + 3] into the image slot of a Q4_0 block (lanes 8 k .. 8 k + 7 hold
+// the 8 float4 of block k, i % 8 == lane % 8): the sum over the block in a fixed shuffle tree, the
+// block's -8 sum(x) stored by its first lane; valid: i < n / 4 (the 8 lanes agree)
+__device__ __forceinline__ float4 gq4_stage(float4 v, const int i, const bool valid, float4* xs4, const int n) {
+    const float t = group_reduce<8>((v.x + v.y) + (v.z + v.w));  // DPP: no LDS round trips
+    if (valid && (i & 7) == 0) ((float*)gq4_nxs(xs4, n))[i >> 3] = -8.f * t;
+    const float f = (i & 4) ? 0.0625f : 1.f;  // elements 16..31 of the block: x / 16 (exact)
+    v.x *= f; v.y *= f; v.z *= f; v.w *= f;
+    return v;
+}
+
 // x (optionally rms-normalised and weighted) -> LDS image xs4, permuted so that lane l at
 // chunk `it` finds the E/4 float4 it multiplies at xs4[(it*E/4 + q)*64 + l].
 // SC1: x was published inside the running launch (write-through): read it with sc1 loads.
-template <int E, int PRO, int THREADS, bool SC1 = false>
+template <int E, int PRO, int THREADS, bool SC1 = false, bool GQ4 = false>
 __device__ __forceinline__ void stage_x(const GemvArgs& a, float4* xs4, float* red) {
     const int n = a.n;
     float scale = 1.f;
@@ -201,6 +220,7 @@ __device__ __forceinline__ void stage_x(const GemvArgs& a, float4* xs4, float* r
             v.z = v.z * scale * w.z;
             v.w = v.w * scale * w.w;
         }
+        if constexpr (GQ4) v = gq4_stage(v, i, true, xs4, n);
         const int c = i << 2;
         const int it = c / (64 * E);
         const int rem = c - it * 64 * E;
@@ -425,31 +445,39 @@ __device__ __forceinline__ float gq_dot(const u32x4 w, const float4* xv) {
             s = fma_mix_hi(p23, xv[i].w, s);
         }
     } else {
-        // Q4_0: byte j = element j (low nibble) | element j + 16 (high); 1024 + n - 1032 = n - 8
-        const h2_t c = __builtin_bit_cast(h2_t, 0xE408E408u);
+        // Q4_0 (byte j = element j in the low nibble, j + 16 in the high one), denormal form: the
+        // nibbles are masked into the mantissa bits of packed f16 with a zero exponent, so each
+        // f16 reads n * 2^-24 exactly (low nibbles of bytes 0 / 2, and of bytes 1 / 3 after >> 8)
+        // or 16 n * 2^-24 (high nibbles in place, against the image's x / 16 for elements 16..31,
+        // exact): 13 VALU ops per 8 elements instead of 19.  The result is sum(n x) * 2^-24; the
+        // caller forms sum((n - 8) x) = 2^24 * s - 8 * sum(x) with the block's staged -8 sum(x).
 #pragma unroll
         for (int i = 0; i < 4; i++) {
-            const uint32_t lo = ww[i] & 0x0F0F0F0Fu, hi = (ww[i] >> 4) & 0x0F0F0F0Fu;
-            const uint32_t l01 = gq_pair(lo, 0x04010400u, c), l23 = gq_pair(lo, 0x04030402u, c);
-            const uint32_t h01 = gq_pair(hi, 0x04010400u, c), h23 = gq_pair(hi, 0x04030402u, c);
-            s = fma_mix_lo(l01, xv[i].x, s);
-            s = fma_mix_hi(l01, xv[i].y, s);
-            s = fma_mix_lo(l23, xv[i].z, s);
-            s = fma_mix_hi(l23, xv[i].w, s);
-            s = fma_mix_lo(h01, xv[4 + i].x, s);
-            s = fma_mix_hi(h01, xv[4 + i].y, s);
-            s = fma_mix_lo(h23, xv[4 + i].z, s);
-            s = fma_mix_hi(h23, xv[4 + i].w, s);
+            const uint32_t w8 = ww[i] >> 8;
+            const uint32_t a = ww[i] & 0x000F000Fu, b = w8 & 0x000F000Fu;
+            const uint32_t c = ww[i] & 0x00F000F0u, d = w8 & 0x00F000F0u;
+            s = fma_mix_lo(a, xv[i].x, s);
+            s = fma_mix_lo(b, xv[i].y, s);
+            s = fma_mix_hi(a, xv[i].z, s);
+            s = fma_mix_hi(b, xv[i].w, s);
+            s = fma_mix_lo(c, xv[4 + i].x, s);
+            s = fma_mix_lo(d, xv[4 + i].y, s);
+            s = fma_mix_hi(c, xv[4 + i].z, s);
+            s = fma_mix_hi(d, xv[4 + i].w, s);
         }
     }
     return s;
 }
 
-// acc[r] += d[r] * sum(q * x) for the ROWS rows of one chunk
+// acc[r] += d[r] * sum(q * x) for the ROWS rows of one chunk (Q4_0: nx = -8 sum(x) of the block)
 template <int DT, int ROWS>
-__device__ __forceinline__ void gq_rows(const u32x4 (&w)[ROWS], const float (&d)[ROWS], const float4* xv, float* acc) {
+__device__ __forceinline__ void gq_rows(const u32x4 (&w)[ROWS], const float (&d)[ROWS], const float4* xv, float* acc,
+                                        const float nx) {
 #pragma unroll
-    for (int r = 0; r < ROWS; r++) acc[r] = fmaf(d[r], gq_dot<DT>(w[r], xv), acc[r]);
+    for (int r = 0; r < ROWS; r++) {
+        if constexpr (DT == XH_Q4_0) acc[r] = fmaf(d[r], fmaf(gq_dot<DT>(w[r], xv), 0x1p24f, nx), acc[r]);
+        else acc[r] = fmaf(d[r], gq_dot<DT>(w[r], xv), acc[r]);
+    }
 }
 
 // gguf blocks (WScale<DT>::BLOCK = 32): chunks [it, it+U) as gemv_chunk, and each chunk's f16
@@ -458,7 +486,8 @@ __device__ __forceinline__ void gq_rows(const u32x4 (&w)[ROWS], const float (&d)
 // same sum up to f32 reassociation)
 template <int DT, int ROWS, int U, bool NT>
 __device__ __forceinline__ void gemv_chunk_gq(const char* wrow, const size_t row_bytes, const size_t qbytes,
-                                              const float4* xs4, const int it, const int lane, float* acc) {
+                                              const float4* xs4, const int it, const int lane, float* acc,
+                                              const float* nxs) {
     constexpr int E = WDec<DT>::E;
     constexpr int QN = E / 4;
     u32x4 wv[U][ROWS];
@@ -477,7 +506,7 @@ __device__ __forceinline__ void gemv_chunk_gq(const char* wrow, const size_t row
         float4 xv[QN];
 #pragma unroll
         for (int qd = 0; qd < QN; qd++) xv[qd] = xs4[((it + u) * QN + qd) * 64 + lane];
-        gq_rows<DT, ROWS>(wv[u], d[u], xv, acc);
+        gq_rows<DT, ROWS>(wv[u], d[u], xv, acc, gq4_image<DT>() ? nxs[(it + u) * 64 + lane] : 0.f);
     }
 }
 
@@ -499,14 +528,14 @@ __device__ __forceinline__ void gq_load_scales(float (&d)[U][ROWS], const char* 
 // ...and the scaled chunk sums against the staged x, as gemv_chunk_gq
 template <int DT, int ROWS, int U>
 __device__ __forceinline__ void gq_compute(const u32x4 (&wv)[U][ROWS], const float (&d)[U][ROWS], const float4* xs4,
-                                           const int it, const int lane, float* acc) {
+                                           const int it, const int lane, float* acc, const float* nxs) {
     constexpr int QN = WDec<DT>::E / 4;
 #pragma unroll
     for (int u = 0; u < U; u++) {
         float4 xv[QN];
 #pragma unroll
         for (int qd = 0; qd < QN; qd++) xv[qd] = xs4[((it + u) * QN + qd) * 64 + lane];
-        gq_rows<DT, ROWS>(wv[u], d[u], xv, acc);
+        gq_rows<DT, ROWS>(wv[u], d[u], xv, acc, gq4_image<DT>() ? nxs[(it + u) * 64 + lane] : 0.f);
     }
 }
 
@@ -550,11 +579,14 @@ __device__ __forceinline__ void gemv_group(const GemvArgs& a, const int g, const
     }
     if constexpr (WScale<DT>::BLOCK > 0) {
         const size_t qb = gq_qbytes(DT, (size_t)n);
-        for (; it + U <= n_full; it += U) gemv_chunk_gq<DT, ROWS, U, S::NT>(wrow, rstride, qb, xs4, it, lane, acc);
+        const float* nxs = gq4_image<DT>() ? gq4_nxs(xs4, n) : nullptr;
+        for (; it + U <= n_full; it += U) gemv_chunk_gq<DT, ROWS, U, S::NT>(wrow, rstride, qb, xs4, it, lane, acc, nxs);
         if (U > 2)
-            for (; it + 2 <= n_full; it += 2) gemv_chunk_gq<DT, ROWS, 2, S::NT>(wrow, rstride, qb, xs4, it, lane, acc);
-        for (; it < n_full; it++) gemv_chunk_gq<DT, ROWS, 1, S::NT>(wrow, rstride, qb, xs4, it, lane, acc);
-        if (it < n_it && (it * 64 + lane) * E < n) gemv_chunk_gq<DT, ROWS, 1, S::NT>(wrow, rstride, qb, xs4, it, lane, acc);
+            for (; it + 2 <= n_full; it += 2)
+                gemv_chunk_gq<DT, ROWS, 2, S::NT>(wrow, rstride, qb, xs4, it, lane, acc, nxs);
+        for (; it < n_full; it++) gemv_chunk_gq<DT, ROWS, 1, S::NT>(wrow, rstride, qb, xs4, it, lane, acc, nxs);
+        if (it < n_it && (it * 64 + lane) * E < n)
+            gemv_chunk_gq<DT, ROWS, 1, S::NT>(wrow, rstride, qb, xs4, it, lane, acc, nxs);
     } else {
         for (; it + U <= n_full; it += U) gemv_chunk<DT, ROWS, U, S::NT>(wrow, rstride, xs4, it, lane, acc);
         if (U > 2)
@@ -653,7 +685,7 @@ __device__ __forceinline__ void gemv_rows_pipe(const GemvArgs& a, const int g0, 
     auto step = [&](const u32x4 (&w)[U][ROWS], const float (&d)[U][ROWS], const float (&f)[ROWS], const int k) {
         const int q = k / steps;
         const int it = (k - q * steps) * U;
-        if constexpr (GQ) gq_compute<DT, ROWS, U>(w, d, xs4, it, lane, acc);
+        if constexpr (GQ) gq_compute<DT, ROWS, U>(w, d, xs4, it, lane, acc, gq4_image<DT>() ? gq4_nxs(xs4, a.n) : nullptr);
         else gemv_compute<DT, ROWS, U>(w, xs4, it, lane, acc);
         if (it + U == steps * U) {
 #pragma unroll
@@ -732,7 +764,7 @@ __device__ __forceinline__ void stage_x_issue(const GemvArgs& a, float4 (&xv)[S:
 // the same value) and the permuted LDS image.  Branch-free like part 1 (a branch would let the
 // compiler sink a load to its use and wait for the weights too): clamped duplicates are
 // masked out of the sum and store the same value to the same slot.
-template <int E, int PRO, class S>
+template <int E, int PRO, class S, bool GQ4 = false>
 __device__ __forceinline__ void stage_x_finish(const GemvArgs& a, const float4 (&xv)[S::XN], const float4 (&nw)[S::XN],
                                                float4* xs4, float* red) {
     const int n4 = a.n >> 2;
@@ -774,6 +806,7 @@ __device__ __forceinline__ void stage_x_finish(const GemvArgs& a, const float4 (
             v.z = v.z * scale * nw[j].z;
             v.w = v.w * scale * nw[j].w;
         }
+        if constexpr (GQ4) v = gq4_stage(v, i, (int)threadIdx.x + j * S::THREADS < n4, xs4, a.n);
         const int c = i << 2;
         const int it = c / (64 * E);
         const int rem = c - it * 64 * E;
@@ -824,7 +857,7 @@ __device__ __forceinline__ void gemv_body(const GemvArgs& a, const int block, co
             const char* wrow = gemv_row_ptr<S::ROWS>(a, min(g, n_groups - 1), lane, rs);
             gq_load_scales<DT, S::ROWS, S::U>(pre_d, wrow, rs, gq_qbytes(DT, (size_t)a.n), 0, lane);
         }
-        stage_x_finish<E, PRO, S>(a, xv, nw, xs4, red);
+        stage_x_finish<E, PRO, S, gq4_image<DT>()>(a, xv, nw, xs4, red);
         if (EPI == EPI_QKV && block == 0) rotate_sinks<S::THREADS>(a, a.sp->kv_sink);
         __syncthreads();
         if (a.trace && threadIdx.x == 0) a.trace[4 * block + 1] = __builtin_amdgcn_s_memrealtime();
@@ -835,7 +868,7 @@ __device__ __forceinline__ void gemv_body(const GemvArgs& a, const int block, co
             else gemv_rows<DT, EPI, S, false, SC1>(a, g, n_blocks * S::WAVES, lane, xs4, pre, &best);
         }
     } else {
-        stage_x<E, PRO, S::THREADS>(a, xs4, red);
+        stage_x<E, PRO, S::THREADS, false, gq4_image<DT>()>(a, xs4, red);
         if (EPI == EPI_QKV && block == 0) rotate_sinks<S::THREADS>(a, a.sp->kv_sink);
         __syncthreads();
         if (a.trace && threadIdx.x == 0) a.trace[4 * block + 1] = __builtin_amdgcn_s_memrealtime();
@@ -875,7 +908,8 @@ template <int DT, class S>
 inline size_t gemv_smem_bytes(const int n) {
     constexpr int E = WDec<DT>::E;
     const int n_it = (n + 64 * E - 1) / (64 * E);
-    return LDS_HEAD_BYTES + (size_t)n_it * 64 * E * sizeof(float);
+    // Q4_0: -8 sum(x) per 32-element block after the image (gq4_nxs)
+    return LDS_HEAD_BYTES + (size_t)n_it * 64 * E * sizeof(float) + (gq4_image<DT>() ? (size_t)n_it * 64 * sizeof(float) : 0);
 }
 // balanced rounds: at most max_blocks * WAVES waves, each with the same group count
 template <class S>

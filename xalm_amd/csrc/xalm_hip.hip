@@ -389,7 +389,10 @@ int attn_nsplit(int n_kv_heads, int max_seq_len) {
 #endif
     int ns = ATTN_SPLIT_WGS / n_kv_heads;
     if (ns > 128) ns = 128;  // the merge holds <= 2 partials per lane
-    const int cap = (max_seq_len + ATTN_MIN_T - 1) / ATTN_MIN_T;
+#ifndef ATTN_CAP_T
+#define ATTN_CAP_T ATTN_MIN_T
+#endif
+    const int cap = (max_seq_len + ATTN_CAP_T - 1) / ATTN_CAP_T;
     if (ns > cap) ns = cap;
     return ns < 1 ? 1 : ns;
 }
