@@ -195,9 +195,39 @@ static inline __m256 f8x8(const uint8_t* p, const int e5m2) {
     const __m256i u = _mm256_or_si256(sg, e5m2 ? _mm256_slli_epi32(mg, 21) : _mm256_slli_epi32(mg, 20));
     return _mm256_mul_ps(_mm256_castsi256_ps(u), _mm256_set1_ps(e5m2 ? 0x1p112f : 0x1p120f));
 }
+/* one gguf block (quants.py dequantize_blocks, :302-311 / :448-454) as 4 x 8 f32: d * q exact
+ * (q has <= 8 significant bits, d 11); element e of the block in lane e % 8 of register e / 8 */
+static inline void gq_block8(const uint8_t* blk, const int dtype, __m256* v) {
+    const __m256 d = _mm256_set1_ps(xo_f16_to_f32((uint16_t)(blk[0] | (blk[1] << 8))));
+    if (dtype == XH_Q8_0) {
+        for (int r = 0; r < 4; r++)
+            v[r] = _mm256_mul_ps(_mm256_cvtepi32_ps(_mm256_cvtepi8_epi32(_mm_loadl_epi64((const __m128i*)(blk + 2 + 8 * r)))), d);
+        return;
+    }
+    const __m128i b = _mm_loadu_si128((const __m128i*)(blk + 2));
+    const __m128i lo = _mm_and_si128(b, _mm_set1_epi8(15)), hi = _mm_and_si128(_mm_srli_epi16(b, 4), _mm_set1_epi8(15));
+    const __m256i m8 = _mm256_set1_epi32(8);
+    v[0] = _mm256_mul_ps(_mm256_cvtepi32_ps(_mm256_sub_epi32(_mm256_cvtepu8_epi32(lo), m8)), d);
+    v[1] = _mm256_mul_ps(_mm256_cvtepi32_ps(_mm256_sub_epi32(_mm256_cvtepu8_epi32(_mm_srli_si128(lo, 8)), m8)), d);
+    v[2] = _mm256_mul_ps(_mm256_cvtepi32_ps(_mm256_sub_epi32(_mm256_cvtepu8_epi32(hi), m8)), d);
+    v[3] = _mm256_mul_ps(_mm256_cvtepi32_ps(_mm256_sub_epi32(_mm256_cvtepu8_epi32(_mm_srli_si128(hi, 8)), m8)), d);
+}
 static float dot_lanes_avx2(const void* rowp, const float* x, const int n, const int dtype) {
     __m256 a0 = _mm256_setzero_ps(), a1 = _mm256_setzero_ps(), a2 = _mm256_setzero_ps(), a3 = _mm256_setzero_ps();
     int j = 0;
+    if (dtype == XH_Q8_0 || dtype == XH_Q4_0) {  /* n % 32 == 0: one block per 32 columns */
+        const uint8_t* row = (const uint8_t*)rowp;
+        const size_t bs = xo_gq_bs(dtype);
+        for (; j + 32 <= n; j += 32) {
+            __m256 v[4];
+            gq_block8(row + (size_t)(j / 32) * bs, dtype, v);
+            a0 = _mm256_fmadd_ps(v[0], _mm256_loadu_ps(x + j), a0);
+            a1 = _mm256_fmadd_ps(v[1], _mm256_loadu_ps(x + j + 8), a1);
+            a2 = _mm256_fmadd_ps(v[2], _mm256_loadu_ps(x + j + 16), a2);
+            a3 = _mm256_fmadd_ps(v[3], _mm256_loadu_ps(x + j + 24), a3);
+        }
+        return hsum8(a0, a1, a2, a3);
+    }
     if (dtype == XH_F16) {
         const uint16_t* row = (const uint16_t*)rowp;
         for (; j + 32 <= n; j += 32) {
@@ -233,6 +263,23 @@ XO_AVX512 static inline __m512 f8x16(const uint8_t* p, const int e5m2) {
 XO_AVX512 static float dot_lanes_avx512(const void* rowp, const float* x, const int n, const int dtype) {
     __m512 b0 = _mm512_setzero_ps(), b1 = _mm512_setzero_ps();  /* [a0 | a1], [a2 | a3] */
     int j = 0;
+    if (dtype == XH_Q8_0 || dtype == XH_Q4_0) {
+        const uint8_t* row = (const uint8_t*)rowp;
+        const size_t bs = xo_gq_bs(dtype);
+        for (; j + 32 <= n; j += 32) {
+            __m256 v[4];
+            gq_block8(row + (size_t)(j / 32) * bs, dtype, v);
+            const __m512 v01 = _mm512_castpd_ps(_mm512_insertf64x4(_mm512_castpd256_pd512(_mm256_castps_pd(v[0])),
+                                                                   _mm256_castps_pd(v[1]), 1));
+            const __m512 v23 = _mm512_castpd_ps(_mm512_insertf64x4(_mm512_castpd256_pd512(_mm256_castps_pd(v[2])),
+                                                                   _mm256_castps_pd(v[3]), 1));
+            b0 = _mm512_fmadd_ps(v01, _mm512_loadu_ps(x + j), b0);
+            b1 = _mm512_fmadd_ps(v23, _mm512_loadu_ps(x + j + 16), b1);
+        }
+        const __m256 h0 = _mm256_castpd_ps(_mm512_extractf64x4_pd(_mm512_castps_pd(b0), 1));
+        const __m256 h1 = _mm256_castpd_ps(_mm512_extractf64x4_pd(_mm512_castps_pd(b1), 1));
+        return hsum8(_mm512_castps512_ps256(b0), h0, _mm512_castps512_ps256(b1), h1);
+    }
     if (dtype == XH_F16) {
         const uint16_t* row = (const uint16_t*)rowp;
         for (; j + 32 <= n; j += 32) {
@@ -288,6 +335,14 @@ void xo_matmul(float* xout, const float* x, const void* w, const int dtype, cons
         const size_t esz = dtype == XH_F16 ? 2 : 1;
 #pragma omp parallel for schedule(static)
         for (i = 0; i < d; i++) xout[i] = dot_lanes((const char*)w + (size_t)i * n * esz, x, n, dtype);
+        return;
+    }
+    if (xo_gq(dtype) && !scalar_order && n % 32 == 0) {
+        /* gguf blocks dequantized 32 at a time (exact), then the lanes order of the f32 loop */
+        pick_isa();
+        const size_t rb = (size_t)n / 32 * xo_gq_bs(dtype);
+#pragma omp parallel for schedule(static)
+        for (i = 0; i < d; i++) xout[i] = dot_lanes((const char*)w + (size_t)i * rb, x, n, dtype);
         return;
     }
 #endif

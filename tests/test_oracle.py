@@ -171,10 +171,13 @@ sys.path.insert(0, sys.argv[1])
 from oracle import oracle as O
 rng = np.random.default_rng(3)
 out = {}
-for dt in (2, 6, 7):
+for dt in (2, 6, 7, 20, 21):
     n, d = 4096 + 40, 48
     if dt == 2:
         w = rng.standard_normal((d, n)).astype(np.float16).view(np.uint16)
+    elif dt in (20, 21):  # gguf Q8_0 / Q4_0 blocks of the converter's quantizer (n % 32 == 0)
+        n = 4096 + 64
+        w = O.quantize_gq(dt, (0.02 * rng.standard_normal((d, n))).astype(np.float32))
     else:
         w = rng.integers(0, 256, (d, n), dtype=np.uint8)
     x = rng.standard_normal(n).astype(np.float32)
@@ -186,7 +189,7 @@ print(O.isa(), out)
 
 
 def test_lanes_order_same_bits_on_every_isa():
-    """The lanes-order matvec (f16, e4m3, e5m2) picks AVX-512 or AVX2 at run time
+    """The lanes-order matvec (f16, e4m3, e5m2, gguf Q8_0 / Q4_0) picks AVX-512 or AVX2 at run time
     (-march=native); both forms must give the same bits, so the timed CPU
     baseline and the parity tests' f32 evaluation are one algorithm on any host."""
     import subprocess
@@ -201,3 +204,28 @@ def test_lanes_order_same_bits_on_every_isa():
         runs.append((int(isa), res))
     assert runs[1][0] == 1
     assert runs[0][1] == runs[1][1]
+
+
+@pytest.mark.parametrize("dt", [L.Q8_0, L.Q4_0])
+def test_gguf_matvec_orders(dt):
+    """gguf matvec (quants.py blocks dequantized exactly, then the reference's f32 row loop):
+    the vectorised lanes order (default) and the sequential order agree with a float64 sum of
+    the dequantized products to f32 accuracy; the sequential order is the scalar loop."""
+    rng = np.random.default_rng(5)
+    n, d = 4096, 64
+    vals = (0.02 * rng.standard_normal((d, n))).astype(np.float32)
+    w = O.quantize_gq(dt, vals)
+    x = rng.standard_normal(n).astype(np.float32)
+    deq = np.array([[O.decode_row(dt, w, r, n, i) for i in range(n)] for r in range(4)], np.float64)
+    ref = deq @ x.astype(np.float64)
+    mag = np.abs(deq) @ np.abs(x.astype(np.float64))
+    outs = []
+    for order in (0, 1):
+        O.set_matmul_order(order)
+        try:
+            outs.append(O.matmul(x, w, dt, n, d))
+        finally:
+            O.set_matmul_order(0)
+    for o in outs:
+        assert np.all(np.abs(o[:4] - ref) <= 1e-5 * mag + 1e-7)
+    assert not np.array_equal(outs[0], outs[1])  # two summation orders, both valid readings

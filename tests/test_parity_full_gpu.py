@@ -87,8 +87,8 @@ def oracle_side(w, c, g, weights, kv):
     f32 orders; teacher-forced on the GPU's tokens so every variant sees the same inputs."""
     res = {}
     for name, prec, order in (("o64", 1, 0), ("lanes", 0, 0), ("seq", 0, 1)):
-        if name == "seq" and w["wdt"] not in (L.F16, L.F8_E4M3, L.F8_E5M2):
-            continue  # bf16 / gguf matmuls have one (sequential) order only: lanes == seq
+        if name == "seq" and w["wdt"] not in (L.F16, L.F8_E4M3, L.F8_E5M2, L.Q8_0, L.Q4_0):
+            continue  # bf16 matmuls have one (sequential) order only: lanes == seq
         O.set_matmul_order(order)
         om = O.OracleModel(c)
         try:
