@@ -4,7 +4,7 @@
 # Each GPU step has its own limit; a crash / abort / timeout ends the run.
 set -u
 cd "$(dirname "$0")/.."
-ROUND=${ROUND:-r05}
+ROUND=${ROUND:-r06}
 PART=${PART:-all}   # a: tests, PMC, kernel trace, fp16 / fp8 benches; b: the other workloads
 OUT=gpurun_out/$ROUND
 mkdir -p "$OUT"
@@ -43,6 +43,11 @@ step kernel_trace_prefill 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_pf"
 cp "$OUT/prof_pf/run_kernel_stats.csv" "$OUT/kernel_stats_prefill.csv"
 step bench 600 python3 bench.py
 step bench_f8 600 python3 bench.py --workload mistral-7b-f8
+# configs[1]'s worst tokens: a synthetic history up to pos 3800, the timed tokens end at kv_len 4096
+step bench_kv4k 300 python3 bench.py --pos0 3800 --prefill-tokens 0
+step kernel_trace_kv4k 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_kv4k" -o run --output-format csv -- \
+    python3 bench.py --pos0 3800 --steps 256 --warmup 8 --no-cpu-baseline --kernel-iters 20 --prefill-tokens 0
+cp "$OUT/prof_kv4k/run_kernel_stats.csv" "$OUT/kernel_stats_kv4k.csv"
 fi
 if [ "$PART" != a ]; then
 step kernel_trace_32k 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_32k" -o run --output-format csv -- \
@@ -61,5 +66,5 @@ step bench_llama 600 python3 bench.py --workload llama3-8b-f16
 step bench_q8_0 600 python3 bench.py --workload mistral-7b-q8_0 --cpu-tokens 16
 step bench_q4_0 600 python3 bench.py --workload mistral-7b-q4_0 --cpu-tokens 16
 fi
-for b in bench bench_f8 bench_32k bench_llama bench_q8_0 bench_q4_0; do [ -f "$OUT/$b.log" ] && tail -1 "$OUT/$b.log" > "$OUT/$b.json"; done
+for b in bench bench_f8 bench_kv4k bench_32k bench_llama bench_q8_0 bench_q4_0; do [ -f "$OUT/$b.log" ] && tail -1 "$OUT/$b.log" > "$OUT/$b.json"; done
 echo "== done"
