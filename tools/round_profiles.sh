@@ -61,10 +61,10 @@ step kernel_trace_q4_0 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_q4" -o
 cp "$OUT/prof_q4/run_kernel_stats.csv" "$OUT/kernel_stats_q4_0.csv"
 step bench_32k 900 python3 bench.py --workload mistral-7b-f16-32k --steps 64 --cpu-tokens 8
 step bench_llama 600 python3 bench.py --workload llama3-8b-f16
-# SURVEY 8f-4 block formats (not BASELINE configs): a shorter CPU sample (the oracle decodes
-# every block element as quants.py does)
-step bench_q8_0 600 python3 bench.py --workload mistral-7b-q8_0 --cpu-tokens 16
-step bench_q4_0 600 python3 bench.py --workload mistral-7b-q4_0 --cpu-tokens 16
+# SURVEY 8f-4 block formats (not BASELINE configs): a shorter CPU sample (the fp64 parity
+# evaluation decodes every block element scalar, as quants.py dequantizes it)
+step bench_q8_0 600 python3 bench.py --workload mistral-7b-q8_0 --cpu-tokens 64
+step bench_q4_0 600 python3 bench.py --workload mistral-7b-q4_0 --cpu-tokens 64
 fi
 for b in bench bench_f8 bench_kv4k bench_32k bench_llama bench_q8_0 bench_q4_0; do [ -f "$OUT/$b.log" ] && tail -1 "$OUT/$b.log" > "$OUT/$b.json"; done
 echo "== done"
