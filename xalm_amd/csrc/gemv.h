@@ -28,14 +28,20 @@ namespace xalm {
 enum { PRO_PLAIN = 0, PRO_RMSNORM = 1 };
 enum { EPI_STORE = 0, EPI_RESID = 1, EPI_QKV = 2, EPI_GLU = 3, EPI_LOGITS = 4 };
 
-constexpr int LDS_HEAD_BYTES = 64;  // block-reduction scratch in front of the x image
+constexpr int LDS_HEAD_BYTES = 64;
+#ifndef GEMV_BAL_CU
+#define GEMV_BAL_CU 256
+#endif  // block-reduction scratch in front of the x image
 
 // attn_wo.h hand-off words of a layer that the launch after it zeroes (every 32nd word)
 constexpr int AW_RESET_WORDS = 9;
 
 // Launch shape of one gemv instance.
-template <int THREADS_, int ROWS_, int U_, bool NT_ = true, int MINW_ = 4, bool PF_ = true, int XN_ = 0, int PIPE_ = 1>
+template <int THREADS_, int ROWS_, int U_, bool NT_ = true, int MINW_ = 4, bool PF_ = true, int XN_ = 0, int PIPE_ = 1,
+          bool BAL_ = false>
 struct GemvShape {
+    static constexpr bool BAL = BAL_;          // grid in whole multiples of the CU count, groups
+                                               // in wave-major order (gemv_blocks, gemv_body)
     static constexpr int PIPE = PIPE_;         // 2: two register sets (gemv_rows_pipe; host-checked
                                                // n % (64 E U) == 0, no gguf blocks)
     static constexpr int THREADS = THREADS_;   // workgroup size
@@ -826,7 +832,9 @@ __device__ __forceinline__ void gemv_body(const GemvArgs& a, const int block, co
     constexpr int E = WDec<DT>::E;
     const int lane = threadIdx.x & 63;
     const int wid = threadIdx.x >> 6;
-    const int g = block * S::WAVES + wid;
+    // BAL: wave-major group order (g = wid * n_blocks + block), so the groups past the last one
+    // fall on the same waves of every workgroup and each CU gets the same share
+    const int g = S::BAL ? wid * n_blocks + block : block * S::WAVES + wid;
 #ifdef GEMV_TRACE_START
     if (a.trace && threadIdx.x == GEMV_TRACE_START * 64) a.trace[4 * block + 3] = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -918,7 +926,14 @@ inline int gemv_blocks(const int rows, const int max_blocks) {
     const int w_max = max_blocks * S::WAVES;
     const int rounds = (n_groups + w_max - 1) / w_max;
     const int waves = (n_groups + rounds - 1) / rounds;
-    return (waves + S::WAVES - 1) / S::WAVES;
+    const int blocks = (waves + S::WAVES - 1) / S::WAVES;
+    // BAL: whole multiples of the CU count, so every CU holds the same number of workgroups
+    // (448 blocks of 8 waves put 2 on 192 CUs and 1 on 64)
+    if (S::BAL && blocks > GEMV_BAL_CU / 2) {
+        const int up = (blocks + GEMV_BAL_CU - 1) / GEMV_BAL_CU * GEMV_BAL_CU;
+        if (up <= max_blocks) return up;
+    }
+    return blocks;
 }
 
 }  // namespace xalm

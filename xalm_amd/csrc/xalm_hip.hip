@@ -283,6 +283,12 @@ using ShapeW2K = GemvShape<1024, 1, UNROLL, true, 4, true, 4, 1>;  // n <= 16384
 #ifndef W2_T1024
 #define W2_T1024 1
 #endif
+#ifndef GEMV_BAL_GQ_GLU
+#define GEMV_BAL_GQ_GLU 1
+#endif
+#ifndef GEMV_BAL_FP8_QKV
+#define GEMV_BAL_FP8_QKV 1
+#endif
 
 
 template <int DT, int PRO, int EPI>
@@ -297,6 +303,13 @@ void launch_gemv_t(const GemvArgs& a, hipStream_t s, int max_waves) {
             if (pf && a.n / 4 <= 3 * 384 && a.n % (64 * E * UNROLL) == 0)
                 return launch_gemv_s<DT, PRO, EPI, ShapeQ384>(a, s, 3 * (max_waves / 2));
         }
+        if constexpr (EPI == EPI_QKV && E >= 16 && GEMV_BAL_FP8_QKV) {
+            // one-byte qkv rows: 3072 one-step groups, 512 workgroups of 6 busy waves (fp8 qkv
+            // 7.3 -> 7.1 us, decode +0.5 %, profiles/r06_decode_ab.txt ab9)
+            using ShapePF2PB = GemvShape<512, ROWS, UNROLL, true, 4, true, 2, 2, true>;
+            if (pf && a.n / 4 <= 2 * 512 && a.n % (64 * E * UNROLL) == 0)
+                return launch_gemv_s<DT, PRO, EPI, ShapePF2PB>(a, s, max_waves);
+        }
         if (pf && a.n / 4 <= 2 * 512 && a.n % (64 * E * UNROLL) == 0)
             return launch_gemv_s<DT, PRO, EPI, ShapePF2P>(a, s, max_waves);
     }
@@ -305,7 +318,8 @@ void launch_gemv_t(const GemvArgs& a, hipStream_t s, int max_waves) {
         // Q4_0 rows of a 4096-wide input are 2 chunks, so 2 chunks per step; W2-long inputs
         // (14336: 14 / 7 chunks per row) step by 2 (Q8_0) / 1 (Q4_0) chunks
         constexpr int UG = DT == XH_Q4_0 ? 2 : UNROLL;
-        using ShapeGQ = GemvShape<512, ROWS, UG, true, 4, true, 2, 2>;
+        // W1/W3 (GEMV_BAL_GQ_GLU): balanced grid, Q4_0 15.0 -> 14.0 us (profiles/r06_decode_ab.txt ab8)
+        using ShapeGQ = GemvShape<512, ROWS, UG, true, 4, true, 2, 2, EPI == EPI_GLU && GEMV_BAL_GQ_GLU>;
         if (a.n % 4 == 0 && a.n / 4 <= 2 * 512 && a.n % (64 * E * UG) == 0)
             return launch_gemv_s<DT, PRO, EPI, ShapeGQ>(a, s, max_waves);
         if constexpr (PRO == PRO_PLAIN) {
