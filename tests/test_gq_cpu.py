@@ -36,19 +36,32 @@ def test_oracle_decode_matches_quants_py(name):
 
 @pytest.mark.parametrize("name", list(TYPES))
 def test_oracle_matmul_uses_the_dequantized_rows(name):
-    # xo_matmul over blocks == the reference row loop over quants.py's dequantized floats
+    # xo_matmul over blocks == the reference row loop over quants.py's dequantized floats: the
+    # sequential order against that loop in float32, the default lanes order (blocks dequantized
+    # 32 at a time, 8-wide FMA lanes) against a float64 sum within f32 accumulation error
     q, deq = G[name], G[name + "_deq"]
     x = np.random.default_rng(5).normal(0, 1, deq.shape[1]).astype(np.float32)
-    out = np.zeros(deq.shape[0], np.float32)
     lib = O._load()
-    lib.xo_matmul(O._p(out), O._p(x), O._p(np.ascontiguousarray(q)), TYPES[name], deq.shape[1], deq.shape[0])
-    ref = np.zeros_like(out)
+    outs = {}
+    for order in (1, 0):
+        out = np.zeros(deq.shape[0], np.float32)
+        O.set_matmul_order(order)
+        try:
+            lib.xo_matmul(O._p(out), O._p(x), O._p(np.ascontiguousarray(q)), TYPES[name], deq.shape[1], deq.shape[0])
+        finally:
+            O.set_matmul_order(0)
+        outs[order] = out
+    ref = np.zeros_like(outs[1])
     for r in range(deq.shape[0]):
         v = np.float32(0)
         for j in range(deq.shape[1]):
             v = np.float32(v + deq[r, j] * x[j])
         ref[r] = v
-    assert np.abs(out - ref).max() <= 1e-6 * max(1.0, float(np.abs(ref).max()))
+    assert np.abs(outs[1] - ref).max() <= 1e-6 * max(1.0, float(np.abs(ref).max()))
+    d64 = deq.astype(np.float64)
+    exact = d64 @ x.astype(np.float64)
+    mag = np.abs(d64) @ np.abs(x.astype(np.float64))
+    assert np.all(np.abs(outs[0] - exact) <= 2e-6 * mag + 1e-7)
 
 
 @pytest.mark.parametrize("name", ["tiny_mistral_q8_0", "tiny_mistral_q4_0"])
