@@ -901,6 +901,9 @@ __global__ __launch_bounds__(64) void prefill_fa_kernel(const float* q, const ui
 #endif
 constexpr int FA_TPS = PF_FA_TPS;
 constexpr int FA_NS = FA_TPS >= 2 ? 2 : 3;  // ring stages
+#ifndef PF_FA_ZIGZAG
+#define PF_FA_ZIGZAG 1
+#endif
 #ifndef PF_FA_WAVES
 #define PF_FA_WAVES 4                    // waves per workgroup
 #endif
@@ -932,7 +935,14 @@ __global__ __launch_bounds__(64 * NW, 2) void prefill_fa2_kernel(const float* q,
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int j32 = lane & 31, h = lane >> 5;
     const int g = blockIdx.x;
+#if PF_FA_ZIGZAG
+    // longest query tiles first, then the shortest first: with two workgroups per CU placed in
+    // dispatch order (b and b + CUs), a CU's pair of causal tiles sums to the same length
+    const int ny = gridDim.y, hy = (ny + 1) / 2, y = blockIdx.y;
+    const int tb = (y < hy ? ny - 1 - y : y - hy) * (NW * TPW);
+#else
     const int tb = (gridDim.y - 1 - blockIdx.y) * (NW * TPW);  // longest rows first
+#endif
     const int t0 = tb + wv * TPW;                              // this wave's first token
     const int tq = t0 + j32 / QPK;
     const int tqc = min(tq, n - 1);
