@@ -520,9 +520,10 @@ def main():
         if n > 0:
             cpu = cpu_baseline(w, c, prompt, logits0, seq, n)
 
-    # the W1/W3 launch's exact instantiation (the pipelined PF shape, PIPE = 2)
-    traffic, src = pmc_traffic("void xalm::gemv_kernel<%d, 1, 3, xalm::GemvShape<512, 2, 4, true, 4, true, 2, 2> >"
-                               % w["wdt"])
+    # the W1/W3 launch's instantiation (the pipelined PF shape, PIPE = 2; the name's prefix, so
+    # the trailing GemvShape parameters added since round 6 still match)
+    traffic, src = pmc_traffic("void xalm::gemv_kernel<%d, 1, 3, xalm::GemvShape<512, 2, %d, true, 4, true, 2, 2"
+                               % (w["wdt"], 2 if w["wdt"] == L.Q4_0 else 4))
     roofline = {"bound": "hbm", "achieved": round(k_gbps, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                 "frac": round(k_gbps / HBM_PEAK_GBPS, 4), "traffic": traffic,
                 "traffic_source": src,
