@@ -101,6 +101,11 @@ int main(int argc, char** argv) {
         {"w4o2k2", xalm::mm_f16_kernel_t<32, 2, 12, 128, 2, 4>, xalm::MmCfg<32, 2, 128, 4>::LDS, 128, 256, 2},
         {"w4o2k4", xalm::mm_f16_kernel_t<32, 2, 12, 128, 2, 4>, xalm::MmCfg<32, 2, 128, 4>::LDS, 128, 256, 4},
         {"m16gk2", xalm::mm_f16_kernel_t<64, 2, 12, 128>, xalm::MmCfg<64, 2, 128>::LDS, 128, 512, 2},
+        // 256-token tiles: 8 waves as 4 (tokens) x 2 (rows), each 64 tokens x 128 rows; a third less
+        // L2 -> LDS traffic per MFMA than the 128-token tile
+        {"b256s2", xalm::mm_f16_kernel_t<32, 2, 12, 256, 1, 8>, xalm::MmCfg<32, 2, 256>::LDS, 256},
+        {"b256s3", xalm::mm_f16_kernel_t<32, 3, 12, 256, 1, 8>, xalm::MmCfg<32, 3, 256>::LDS, 256},
+        {"b256s3p", xalm::mm_f16_kernel_t<32, 3, 13, 256, 1, 8>, xalm::MmCfg<32, 3, 256>::LDS, 256},
     };
     const int NV = sizeof vars / sizeof vars[0];
     for (int v = 0; v < NV; v++)
