@@ -1,0 +1,3 @@
+export TMPDIR=/tmp
+bash tools/gpu_step.sh na_tests 600 python3 -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_forward_gpu.py tests/test_regimes_gpu.py && \
+LIBS="base na" WL="mistral-7b-f16 mistral-7b-f8" ROUNDS=3 bash tools/gpu_step.sh na_ab 900 bash tools/abn.sh

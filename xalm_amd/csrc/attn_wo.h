@@ -61,6 +61,52 @@ __host__ __device__ constexpr size_t aw_image_bytes(const int n) {
     return (size_t)((n + 64 * E - 1) / (64 * E)) * 64 * E * sizeof(float);
 }
 
+#ifndef AW_STAGE_NA
+#define AW_STAGE_NA 1
+#endif
+// aw_stage_merged's register path for NA partials: per thread its float4 of each partial and its
+// head's (m, l) pairs (one 8-byte load each), merged in partial order
+template <int E, int HD, int NA, int THREADS>
+__device__ __forceinline__ void aw_stage_na(const AttnArgs& aa, const int n, float4* xs4) {
+    const int nh = aa.n_heads;
+    const size_t stride = (size_t)nh * HD;  // floats per split in part_o
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)aa.part_ml, 0, 0x7fffffff, 0x00020000);
+    for (int i = threadIdx.x; i < (n >> 2); i += THREADS) {
+        const int h = (4 * i) / HD;
+        u32x4 ov[NA];
+        uint32_t mlv[NA][2];
+#pragma unroll
+        for (int j = 0; j < NA; j++) {
+            ov[j] = ld_sc1_x4(aa.part_o, (uint32_t)((j * stride + 4 * (size_t)i) * 4));
+            const auto u = __builtin_amdgcn_raw_buffer_load_b64(rs, (j * nh + h) * 8, 0, 16);  // sc1
+            mlv[j][0] = u[0];
+            mlv[j][1] = u[1];
+        }
+        // out = sum_s e^{m_s-M} o_s / sum_s e^{m_s-M} l_s   (as attention.h's merge)
+        float M = -FLT_MAX;
+#pragma unroll
+        for (int j = 0; j < NA; j++) M = fmaxf(M, bits_f32(mlv[j][0]));
+        float den = 0.f;
+        float4 num = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int j = 0; j < NA; j++) {
+            const float f = expf(bits_f32(mlv[j][0]) - M);
+            den = fmaf(f, bits_f32(mlv[j][1]), den);
+            num.x = fmaf(f, bits_f32(ov[j].x), num.x);
+            num.y = fmaf(f, bits_f32(ov[j].y), num.y);
+            num.z = fmaf(f, bits_f32(ov[j].z), num.z);
+            num.w = fmaf(f, bits_f32(ov[j].w), num.w);
+        }
+        const float4 v = make_float4(num.x / den, num.y / den, num.z / den, num.w / den);
+        const int c = i << 2;
+        const int it = c / (64 * E);
+        const int rem = c - it * 64 * E;
+        const int l = rem / E;
+        const int qd = (rem - l * E) >> 2;
+        xs4[(it * (E / 4) + qd) * 64 + l] = v;
+    }
+}
+
 // x image of the Wo rows = the merged attention output.  Up to AW_MAXS partials (attn_wo.h: longer
 // histories arrive merged, aw_long) every thread loads its float4 of each partial AND its head's
 // (m, l) pairs in one round trip and forms the weights itself (n_active expf per thread): no LDS
@@ -117,6 +163,16 @@ __device__ __forceinline__ void aw_stage_merged(const AttnArgs& aa, const int n,
         }
         return;
     }
+#if AW_STAGE_NA
+    // the partial count as a constant: no clamped duplicate loads (n_active = 1 issued 4 o and
+    // 8 (m, l) loads per thread for 1 and 2 it needs)
+    switch (n_active) {
+        case 1: aw_stage_na<E, HD, 1, THREADS>(aa, n, xs4); return;
+        case 2: aw_stage_na<E, HD, 2, THREADS>(aa, n, xs4); return;
+        case 3: aw_stage_na<E, HD, 3, THREADS>(aa, n, xs4); return;
+        default: aw_stage_na<E, HD, MAXS, THREADS>(aa, n, xs4); return;
+    }
+#else
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)aa.part_ml, 0, 0x7fffffff, 0x00020000);
     for (int i = tid; i < n4; i += THREADS) {
         const int h = (4 * i) / HD;
@@ -155,6 +211,7 @@ __device__ __forceinline__ void aw_stage_merged(const AttnArgs& aa, const int n,
         const int qd = (rem - l * E) >> 2;
         xs4[(it * (E / 4) + qd) * 64 + l] = v;
     }
+#endif
 }
 
 // x image of the Wo rows from the merged attention output (sc1: written in this launch)
