@@ -19,6 +19,8 @@
 
 #include <float.h>
 
+#include <type_traits>
+
 #include "common.h"
 
 namespace xalm {
@@ -413,7 +415,11 @@ __device__ __forceinline__ void attn_block(const AttnArgs& a, const int g, const
     // step and the partial loads share one round trip.
     constexpr int MG = (THREADS / NO < WAVES - 1 ? THREADS / NO : WAVES - 1) > 0
                            ? (THREADS / NO < WAVES - 1 ? THREADS / NO : WAVES - 1) : 1;
-    constexpr int MB = 16;  // partial values per thread per round trip
+    // partial values per thread per round trip: 4 / 8 / 16 by the group's split count (a fixed 16
+    // requested clamped copies of the last split for short chunks)
+#ifndef ATTN_MERGE_MB
+#define ATTN_MERGE_MB 1
+#endif
     float* wts = sc;        // [QPK][n_active] weights (sc is free now)
     float* den_s = red + MG * NO;  // [QPK]; red[k * NO + idx]: group sums
     const int chunk = (n_active + MG - 1) / MG;
@@ -422,13 +428,15 @@ __device__ __forceinline__ void attn_block(const AttnArgs& a, const int g, const
     const int j0 = mgrp * chunk, j1 = min(n_active, j0 + chunk);
     const float* msrc = a.part_o + (size_t)g * NO + midx;
     const size_t mstride = (size_t)a.n_heads * HD;
-    {
+    auto merge = [&](auto mb_c) {
+        constexpr int MB = decltype(mb_c)::value;
+        constexpr int NC = MB >= 16 ? 2 : 1;  // (m, l) loads per lane: up to 64 NC splits
         // (m, l) of head min(wid, QPK - 1), up to 2 splits per lane (n_active <= 128);
         // clamped indices so every load sits in one basic block with the partial loads
         const int h = min(wid, QPK - 1);
         float mv[2], lv[2];
 #pragma unroll
-        for (int c = 0; c < 2; c++) {
+        for (int c = 0; c < NC; c++) {
             const int j = min(lane + 64 * c, n_active - 1);
             const float* mlp = a.part_ml + ((size_t)j * a.n_heads + g * QPK + h) * 2;
             mv[c] = ld_sc1(mlp);
@@ -437,7 +445,8 @@ __device__ __forceinline__ void attn_block(const AttnArgs& a, const int g, const
         float pv[MB];
 #pragma unroll
         for (int k = 0; k < MB; k++) pv[k] = ld_sc1(msrc + (size_t)min(j0 + k, n_active - 1) * mstride);
-        const bool in0 = lane < n_active, in1 = lane + 64 < n_active;
+        if constexpr (NC == 1) { mv[1] = -FLT_MAX; lv[1] = 0.f; }
+        const bool in0 = lane < n_active, in1 = NC > 1 && lane + 64 < n_active;
         const float M = wave_max(fmaxf(in0 ? mv[0] : -FLT_MAX, in1 ? mv[1] : -FLT_MAX));
         const float f0 = expf(mv[0] - M), f1 = expf(mv[1] - M);
         if (wid < QPK) {
@@ -475,7 +484,10 @@ __device__ __forceinline__ void attn_block(const AttnArgs& a, const int g, const
                 red[idx] = n2;
             }
         }
-    }
+    };
+    if (ATTN_MERGE_MB && chunk <= 4) merge(std::integral_constant<int, 4>{});
+    else if (ATTN_MERGE_MB && chunk <= 8) merge(std::integral_constant<int, 8>{});
+    else merge(std::integral_constant<int, 16>{});
     __syncthreads();
     for (int idx = tid; idx < NO; idx += THREADS) {
         float num = red[idx];
